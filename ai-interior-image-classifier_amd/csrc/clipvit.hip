@@ -1,0 +1,635 @@
+// libclipvit_hip.so — host side of the C ABI declared in include/clipvit.h.
+//
+// Owns the device weight store (fp32 masters + packed 16-bit MFMA operands), merges LoRA at
+// load time, keeps the text-feature table, and runs the encoder forward as a fixed sequence of
+// hand-written gfx950 kernels on the caller's stream:
+//
+//   im2col -> GEMM(patch, EPI_PATCH) -> embed+ln_pre+ln_1
+//   12x [ GEMM(qkv) -> attention -> GEMM(out_proj, +residual) -> ln_2
+//         -> GEMM(c_fc, QuickGELU) -> GEMM(c_proj, +residual) -> ln_1(next) ]
+//   -> ln_post(CLS) @ proj -> [classify: L2-norm, 100*cos logits, segment softmax, top-5]
+//
+// Reference call sites replaced: clip.load (main.py:152, 241), encode_image (main.py:204,
+// 444, 503), LoRA injection + loading (main.py:62-113, 247-251), text caches (main.py:179-182,
+// 296-311) and the head (main.py:205-217, 445-459, 504-509).
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "clipvit.h"
+#include "common.h"
+
+using namespace clipvit;
+
+static thread_local std::string g_err;
+
+#define FAIL(code, msg)        \
+    do {                       \
+        g_err = (msg);         \
+        return (code);         \
+    } while (0)
+
+#define HIPCHK(x)                                                                  \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            g_err = std::string(#x) + " failed: " + hipGetErrorString(e_);        \
+            return CLIPVIT_E_HIP;                                                  \
+        }                                                                          \
+    } while (0)
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) hipSetDevice(prev);
+    }
+};
+
+struct LayerW {
+    void *wqkv = nullptr, *wout = nullptr, *wfc = nullptr, *wproj = nullptr;
+    const float *bqkv, *bout, *bfc, *bproj, *ln1g, *ln1b, *ln2g, *ln2b;
+};
+
+struct Workspace {
+    int cap = 0;
+    float* x = nullptr;  // [cap*N, D] fp32 residual stream
+    void* h = nullptr;   // [cap*N, D] 16-bit LN output; also the attention output
+    void* qkv = nullptr; // [cap*N, 3D]
+    void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the im2col buffer
+    float* f = nullptr;  // [cap, E] projected features
+    hipEvent_t done = nullptr;
+    bool used = false;
+};
+
+enum Fam { F_EMBED = 0, F_QKV, F_ATTN, F_OUT, F_LN, F_FC, F_PROJ, F_HEAD, F_COUNT };
+
+struct Prof {
+    std::vector<hipEvent_t> ev;
+    std::vector<int> fam;
+    size_t k = 0;
+    void mark(hipStream_t s, int f) {
+        if (k < ev.size()) {
+            hipEventRecord(ev[k], s);
+            fam[k] = f;
+            ++k;
+        }
+    }
+};
+
+}  // namespace
+
+struct clipvit_handle {
+    clipvit_config cfg{};
+    int device = 0;
+    int G = 0, G2 = 0, N = 0, D = 0, E = 0, K3 = 0, Kp = 0, dt = 1;
+    std::unordered_map<std::string, float*> master;
+    std::unordered_map<std::string, std::vector<int64_t>> shapes;
+    std::vector<std::string> order;
+    void* wpatch = nullptr;
+    std::vector<LayerW> layers;
+    float* scratch = nullptr;
+    size_t scratch_elems = 0;
+    bool loaded = false;
+    // cached pointers into `master` (read concurrently by forward(); never via operator[])
+    const float *cls = nullptr, *pos = nullptr, *lnpre_g = nullptr, *lnpre_b = nullptr;
+    const float *lnpost_g = nullptr, *lnpost_b = nullptr, *proj = nullptr;
+    float* Tt = nullptr;
+    int C = 0, Cpad = 0, nseg = 0;
+    int* seg_dev = nullptr;
+    std::vector<int> seg_host;
+    std::mutex mu;
+    std::vector<Workspace*> pool;
+    int var[5] = {0, 0, 0, 0, 0};  // GEMM tile variants: qkv, out, fc, proj, patch
+};
+
+static std::string L(int i, const char* leaf) {
+    return "visual.transformer.resblocks." + std::to_string(i) + "." + leaf;
+}
+
+static void expected_tensors(const clipvit_handle* h,
+                             std::vector<std::pair<std::string, std::vector<int64_t>>>& out) {
+    const int64_t D = h->D, P = h->cfg.patch_size;
+    out.push_back({"visual.conv1.weight", {D, 3, P, P}});
+    out.push_back({"visual.class_embedding", {D}});
+    out.push_back({"visual.positional_embedding", {h->N, D}});
+    out.push_back({"visual.ln_pre.weight", {D}});
+    out.push_back({"visual.ln_pre.bias", {D}});
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        out.push_back({L(i, "ln_1.weight"), {D}});
+        out.push_back({L(i, "ln_1.bias"), {D}});
+        out.push_back({L(i, "attn.in_proj_weight"), {3 * D, D}});
+        out.push_back({L(i, "attn.in_proj_bias"), {3 * D}});
+        out.push_back({L(i, "attn.out_proj.weight"), {D, D}});
+        out.push_back({L(i, "attn.out_proj.bias"), {D}});
+        out.push_back({L(i, "ln_2.weight"), {D}});
+        out.push_back({L(i, "ln_2.bias"), {D}});
+        out.push_back({L(i, "mlp.c_fc.weight"), {4 * D, D}});
+        out.push_back({L(i, "mlp.c_fc.bias"), {4 * D}});
+        out.push_back({L(i, "mlp.c_proj.weight"), {D, 4 * D}});
+        out.push_back({L(i, "mlp.c_proj.bias"), {D}});
+    }
+    out.push_back({"visual.ln_post.weight", {D}});
+    out.push_back({"visual.ln_post.bias", {D}});
+    out.push_back({"visual.proj", {D, (int64_t)h->E}});
+}
+
+static int free_ws(Workspace* w) {
+    if (!w) return 0;
+    hipFree(w->x);
+    hipFree(w->h);
+    hipFree(w->qkv);
+    hipFree(w->u);
+    hipFree(w->f);
+    if (w->done) hipEventDestroy(w->done);
+    delete w;
+    return 0;
+}
+
+static int alloc_ws(clipvit_handle* h, Workspace** out) {
+    Workspace* w = new Workspace();
+    w->cap = h->cfg.max_batch;
+    const size_t rows = (size_t)w->cap * h->N;
+    const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)w->cap * h->G2 * h->Kp * 2);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&w->x, rows * h->D * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&w->h, rows * h->D * 2);
+    if (e == hipSuccess) e = hipMalloc(&w->qkv, rows * 3 * h->D * 2);
+    if (e == hipSuccess) e = hipMalloc(&w->u, ubytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&w->f, (size_t)w->cap * h->E * sizeof(float));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        free_ws(w);
+        g_err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
+        return CLIPVIT_E_NOMEM;
+    }
+    *out = w;
+    return 0;
+}
+
+// Take a free workspace (allocating one if every pooled workspace is busy) and order the
+// caller's stream after that workspace's previous user.
+static int acquire_ws(clipvit_handle* h, hipStream_t s, Workspace** out) {
+    Workspace* w = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        for (auto* c : h->pool)
+            if (c && !c->used) {
+                w = c;
+                break;
+            }
+        if (w) w->used = true;
+    }
+    if (!w) {
+        int rc = alloc_ws(h, &w);
+        if (rc) return rc;
+        w->used = true;
+        std::lock_guard<std::mutex> lk(h->mu);
+        h->pool.push_back(w);
+    }
+    HIPCHK(hipStreamWaitEvent(s, w->done, 0));
+    *out = w;
+    return 0;
+}
+
+static void release_ws(clipvit_handle* h, hipStream_t s, Workspace* w) {
+    hipEventRecord(w->done, s);
+    std::lock_guard<std::mutex> lk(h->mu);
+    w->used = false;
+}
+
+static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
+                const float* bias, void* C, int M, int N, int K, int ldc, int variant) {
+    GemmArgs a{};
+    a.A = A; a.W = W; a.bias = bias; a.C = C;
+    a.M = M; a.N = N; a.K = K; a.ldc = ldc;
+    a.patch_g2 = h->G2; a.patch_ntok = h->N;
+    if (launch_gemm(s, h->dt, epi, a, variant) != 0) {
+        g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
+                " K=" + std::to_string(K);
+        return CLIPVIT_E_INVALID;
+    }
+    return 0;
+}
+
+// Encoder forward for B images; writes the projected (un-normalised) features to f_out.
+static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
+                   Workspace* w, float* f_out, Prof* prof) {
+    const int D = h->D, N = h->N, M = B * N;
+    int rc;
+    if (prof) prof->mark(s, F_EMBED);
+    launch_im2col(s, in_dtype, h->dt, pix, w->u, B, h->cfg.image_size, h->cfg.patch_size, h->Kp);
+    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, h->var[4]);
+    if (rc) return rc;
+    const LayerW& l0 = h->layers[0];
+    launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
+                    B, N, D);
+    if (prof) prof->mark(s, F_EMBED);
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        const LayerW& ly = h->layers[i];
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, h->var[0])))
+            return rc;
+        if (prof) prof->mark(s, F_QKV);
+        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        if (prof) prof->mark(s, F_ATTN);
+        if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, h->var[1])))
+            return rc;
+        if (prof) prof->mark(s, F_OUT);
+        launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
+        if (prof) prof->mark(s, F_LN);
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, h->var[2])))
+            return rc;
+        if (prof) prof->mark(s, F_FC);
+        if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, h->var[3])))
+            return rc;
+        if (prof) prof->mark(s, F_PROJ);
+        if (i + 1 < h->cfg.layers) {
+            launch_layernorm(s, h->dt, w->x, w->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+            if (prof) prof->mark(s, F_LN);
+        }
+    }
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    if (prof) prof->mark(s, F_HEAD);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+static int check_call(clipvit_handle* h, const void* pix, int dtype, int B) {
+    if (!h) FAIL(CLIPVIT_E_INVALID, "null handle");
+    if (!h->loaded) FAIL(CLIPVIT_E_STATE, "weights not loaded");
+    if (!pix) FAIL(CLIPVIT_E_INVALID, "null pixel buffer");
+    if (dtype < 0 || dtype > 2) FAIL(CLIPVIT_E_INVALID, "bad pixel dtype");
+    if (B <= 0 || B > h->cfg.max_batch)
+        FAIL(CLIPVIT_E_INVALID, "batch " + std::to_string(B) + " outside [1, max_batch=" +
+                                    std::to_string(h->cfg.max_batch) + "]");
+    return 0;
+}
+
+// Re-pack every Linear from its fp32 master (optionally with merged LoRA deltas).
+static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name, void* dst,
+                       const float* src) {
+    const auto& sh = h->shapes[name];
+    const int N = (int)sh[0];
+    int K = 1;
+    for (size_t i = 1; i < sh.size(); ++i) K *= (int)sh[i];
+    const int Kp = (K + 63) / 64 * 64;
+    launch_pack_weight(s, h->dt, src ? src : h->master[name], dst, N, K, Kp);
+    return 0;
+}
+
+extern "C" {
+
+const char* clipvit_last_error(void) { return g_err.c_str(); }
+int clipvit_abi_version(void) { return CLIPVIT_ABI_VERSION; }
+
+int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) {
+    g_err.clear();
+    if (!cfg || !out) FAIL(CLIPVIT_E_INVALID, "null argument");
+    const clipvit_config& c = *cfg;
+    if (c.patch_size <= 0 || c.image_size % c.patch_size)
+        FAIL(CLIPVIT_E_INVALID, "image_size must be a multiple of patch_size");
+    if (c.width % 256 || c.width < 512 || c.width > 1280)
+        FAIL(CLIPVIT_E_INVALID, "width must be a multiple of 256 in [512, 1280]");
+    if (c.heads * 64 != c.width) FAIL(CLIPVIT_E_INVALID, "heads * 64 must equal width");
+    if (c.embed_dim % 64 || c.embed_dim <= 0) FAIL(CLIPVIT_E_INVALID, "embed_dim % 64 != 0");
+    if (c.compute_dtype != CLIPVIT_BF16 && c.compute_dtype != CLIPVIT_F16)
+        FAIL(CLIPVIT_E_INVALID, "compute_dtype must be BF16 or F16");
+    if (c.layers <= 0 || c.max_batch <= 0) FAIL(CLIPVIT_E_INVALID, "layers/max_batch must be > 0");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) FAIL(CLIPVIT_E_INVALID, "bad device index");
+    DeviceGuard dg(device);
+    auto* h = new clipvit_handle();
+    h->cfg = c;
+    h->device = device;
+    h->G = c.image_size / c.patch_size;
+    h->G2 = h->G * h->G;
+    h->N = h->G2 + 1;
+    h->D = c.width;
+    h->E = c.embed_dim;
+    h->K3 = 3 * c.patch_size * c.patch_size;
+    h->Kp = (h->K3 + 63) / 64 * 64;
+    h->dt = c.compute_dtype;
+    if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
+        int k = 0;
+        for (const char* p = v; *p && k < 5; ++k) {
+            h->var[k] = atoi(p);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+    }
+    *out = h;
+    return 0;
+}
+
+int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_t n) {
+    g_err.clear();
+    if (!h || (!tensors && n)) FAIL(CLIPVIT_E_INVALID, "null argument");
+    DeviceGuard dg(h->device);
+    std::unordered_map<std::string, const clipvit_tensor*> byname;
+    for (size_t i = 0; i < n; ++i)
+        if (tensors[i].name) byname[tensors[i].name] = &tensors[i];
+    std::vector<std::pair<std::string, std::vector<int64_t>>> exp;
+    expected_tensors(h, exp);
+    // validate everything before touching the device
+    for (auto& e : exp) {
+        auto it = byname.find(e.first);
+        if (it == byname.end()) FAIL(CLIPVIT_E_INVALID, "missing tensor " + e.first);
+        const clipvit_tensor* t = it->second;
+        bool ok = t->ndim == (int)e.second.size() && t->data;
+        for (int d = 0; ok && d < t->ndim; ++d) ok = t->shape[d] == e.second[d];
+        if (!ok) FAIL(CLIPVIT_E_INVALID, "bad shape/data for " + e.first);
+    }
+    for (auto& e : exp) {
+        const clipvit_tensor* t = byname[e.first];
+        size_t cnt = 1;
+        for (auto d : e.second) cnt *= (size_t)d;
+        float*& dst = h->master[e.first];
+        if (!dst) HIPCHK(hipMalloc(&dst, cnt * sizeof(float)));
+        HIPCHK(hipMemcpy(dst, t->data, cnt * sizeof(float), hipMemcpyHostToDevice));
+        h->shapes[e.first] = e.second;
+    }
+    h->cls = h->master["visual.class_embedding"];
+    h->pos = h->master["visual.positional_embedding"];
+    h->lnpre_g = h->master["visual.ln_pre.weight"];
+    h->lnpre_b = h->master["visual.ln_pre.bias"];
+    h->lnpost_g = h->master["visual.ln_post.weight"];
+    h->lnpost_b = h->master["visual.ln_post.bias"];
+    h->proj = h->master["visual.proj"];
+    // packed operands
+    const size_t D = h->D;
+    auto alloc16 = [&](void*& p, size_t elems) -> hipError_t {
+        if (p) return hipSuccess;
+        return hipMalloc(&p, elems * 2);
+    };
+    HIPCHK(alloc16(h->wpatch, D * h->Kp));
+    h->layers.resize(h->cfg.layers);
+    size_t maxw = D * h->Kp;
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        LayerW& ly = h->layers[i];
+        HIPCHK(alloc16(ly.wqkv, 3 * D * D));
+        HIPCHK(alloc16(ly.wout, D * D));
+        HIPCHK(alloc16(ly.wfc, 4 * D * D));
+        HIPCHK(alloc16(ly.wproj, 4 * D * D));
+        ly.bqkv = h->master[L(i, "attn.in_proj_bias")];
+        ly.bout = h->master[L(i, "attn.out_proj.bias")];
+        ly.bfc = h->master[L(i, "mlp.c_fc.bias")];
+        ly.bproj = h->master[L(i, "mlp.c_proj.bias")];
+        ly.ln1g = h->master[L(i, "ln_1.weight")];
+        ly.ln1b = h->master[L(i, "ln_1.bias")];
+        ly.ln2g = h->master[L(i, "ln_2.weight")];
+        ly.ln2b = h->master[L(i, "ln_2.bias")];
+        maxw = std::max(maxw, 4 * D * D);
+    }
+    if (h->scratch_elems < maxw) {
+        if (h->scratch) hipFree(h->scratch);
+        HIPCHK(hipMalloc(&h->scratch, maxw * sizeof(float)));
+        h->scratch_elems = maxw;
+    }
+    hipStream_t s = nullptr;
+    pack_linear(h, s, "visual.conv1.weight", h->wpatch, nullptr);
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        LayerW& ly = h->layers[i];
+        pack_linear(h, s, L(i, "attn.in_proj_weight"), ly.wqkv, nullptr);
+        pack_linear(h, s, L(i, "attn.out_proj.weight"), ly.wout, nullptr);
+        pack_linear(h, s, L(i, "mlp.c_fc.weight"), ly.wfc, nullptr);
+        pack_linear(h, s, L(i, "mlp.c_proj.weight"), ly.wproj, nullptr);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    if (h->pool.empty()) {
+        Workspace* w = nullptr;
+        int rc = alloc_ws(h, &w);
+        if (rc) return rc;
+        h->pool.push_back(w);
+    }
+    h->loaded = true;
+    return 0;
+}
+
+int clipvit_load_lora(clipvit_handle* h, const clipvit_lora* items, size_t n) {
+    g_err.clear();
+    if (!h || (!items && n)) FAIL(CLIPVIT_E_INVALID, "null argument");
+    if (!h->loaded) FAIL(CLIPVIT_E_STATE, "weights not loaded");
+    DeviceGuard dg(h->device);
+    // map target -> packed destination
+    std::unordered_map<std::string, void*> dst;
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        dst[L(i, "attn.in_proj_weight")] = h->layers[i].wqkv;
+        dst[L(i, "attn.out_proj.weight")] = h->layers[i].wout;
+        dst[L(i, "mlp.c_fc.weight")] = h->layers[i].wfc;
+        dst[L(i, "mlp.c_proj.weight")] = h->layers[i].wproj;
+    }
+    for (size_t k = 0; k < n; ++k) {
+        const clipvit_lora& it = items[k];
+        if (!it.target || !dst.count(it.target))
+            FAIL(CLIPVIT_E_INVALID, std::string("unknown LoRA target ") + (it.target ? it.target : "(null)"));
+        const auto& sh = h->shapes[it.target];
+        if (sh[0] != it.out_features || sh[1] != it.in_features || it.rank <= 0 || !it.A || !it.B)
+            FAIL(CLIPVIT_E_INVALID, std::string("LoRA shape mismatch for ") + it.target);
+    }
+    hipStream_t s = nullptr;
+    // reset every Linear to its base weight, then merge each adapter (last call wins)
+    for (auto& kv : dst) pack_linear(h, s, kv.first, kv.second, nullptr);
+    std::unordered_map<std::string, std::vector<size_t>> groups;
+    for (size_t k = 0; k < n; ++k) groups[items[k].target].push_back(k);
+    for (auto& gkv : groups) {
+        const auto& sh = h->shapes[gkv.first];
+        const size_t cnt = (size_t)sh[0] * sh[1];
+        HIPCHK(hipMemcpy(h->scratch, h->master[gkv.first], cnt * sizeof(float), hipMemcpyDeviceToDevice));
+        for (size_t k : gkv.second) {
+            const clipvit_lora& it = items[k];
+            float *dA = nullptr, *dB = nullptr;
+            HIPCHK(hipMalloc(&dA, (size_t)it.in_features * it.rank * sizeof(float)));
+            HIPCHK(hipMalloc(&dB, (size_t)it.rank * it.out_features * sizeof(float)));
+            HIPCHK(hipMemcpy(dA, it.A, (size_t)it.in_features * it.rank * sizeof(float), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(dB, it.B, (size_t)it.rank * it.out_features * sizeof(float), hipMemcpyHostToDevice));
+            launch_lora_merge(s, h->scratch, dA, dB, it.in_features, it.out_features, it.rank, it.scaling);
+            HIPCHK(hipDeviceSynchronize());
+            hipFree(dA);
+            hipFree(dB);
+        }
+        pack_linear(h, s, gkv.first, dst[gkv.first], h->scratch);
+        HIPCHK(hipDeviceSynchronize());
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipDeviceSynchronize());
+    return 0;
+}
+
+int clipvit_set_text_features(clipvit_handle* h, const float* T, int C, int E, const int* seg_offsets,
+                              int nseg) {
+    g_err.clear();
+    if (!h || !T || !seg_offsets) FAIL(CLIPVIT_E_INVALID, "null argument");
+    if (E != h->E) FAIL(CLIPVIT_E_INVALID, "text feature width != embed_dim");
+    if (C <= 0 || nseg <= 0) FAIL(CLIPVIT_E_INVALID, "empty text table");
+    if (seg_offsets[0] != 0 || seg_offsets[nseg] != C)
+        FAIL(CLIPVIT_E_INVALID, "seg_offsets must start at 0 and end at C");
+    for (int i = 0; i < nseg; ++i)
+        if (seg_offsets[i + 1] <= seg_offsets[i]) FAIL(CLIPVIT_E_INVALID, "empty or unordered segment");
+    DeviceGuard dg(h->device);
+    const int Cpad = (C + 63) / 64 * 64;
+    std::vector<float> tt((size_t)E * Cpad, 0.f);
+    for (int c = 0; c < C; ++c)
+        for (int e = 0; e < E; ++e) tt[(size_t)e * Cpad + c] = T[(size_t)c * E + e];
+    HIPCHK(hipDeviceSynchronize());  // no call may still read the old table
+    if (h->Tt) hipFree(h->Tt);
+    if (h->seg_dev) hipFree(h->seg_dev);
+    h->Tt = nullptr;
+    h->seg_dev = nullptr;
+    HIPCHK(hipMalloc(&h->Tt, tt.size() * sizeof(float)));
+    HIPCHK(hipMemcpy(h->Tt, tt.data(), tt.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&h->seg_dev, (nseg + 1) * sizeof(int)));
+    HIPCHK(hipMemcpy(h->seg_dev, seg_offsets, (nseg + 1) * sizeof(int), hipMemcpyHostToDevice));
+    h->seg_host.assign(seg_offsets, seg_offsets + nseg + 1);
+    h->C = C;
+    h->Cpad = Cpad;
+    h->nseg = nseg;
+    return 0;
+}
+
+int clipvit_text_shape(clipvit_handle* h, int* C, int* nseg) {
+    if (!h) FAIL(CLIPVIT_E_INVALID, "null handle");
+    if (C) *C = h->C;
+    if (nseg) *nseg = h->nseg;
+    return 0;
+}
+
+int clipvit_encode_image(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype, int B,
+                         float* emb_dev) {
+    g_err.clear();
+    int rc = check_call(h, pixels_dev, dtype, B);
+    if (rc) return rc;
+    if (!emb_dev) FAIL(CLIPVIT_E_INVALID, "null output");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    Workspace* w = nullptr;
+    if ((rc = acquire_ws(h, s, &w))) return rc;
+    rc = forward(h, s, pixels_dev, dtype, B, w, emb_dev, nullptr);
+    release_ws(h, s, w);
+    return rc;
+}
+
+int clipvit_classify(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype, int B,
+                     float* emb_dev, float* logits_dev, float* probs_dev, int32_t* top_idx,
+                     float* top_prob) {
+    g_err.clear();
+    int rc = check_call(h, pixels_dev, dtype, B);
+    if (rc) return rc;
+    if (!h->Tt) FAIL(CLIPVIT_E_STATE, "text features not set");
+    if (!logits_dev) FAIL(CLIPVIT_E_INVALID, "null logits buffer");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    Workspace* w = nullptr;
+    if ((rc = acquire_ws(h, s, &w))) return rc;
+    rc = forward(h, s, pixels_dev, dtype, B, w, w->f, nullptr);
+    if (!rc) {
+        launch_logits(s, w->f, h->Tt, emb_dev, logits_dev, B, h->E, h->C, h->Cpad);
+        if (probs_dev || top_idx || top_prob)
+            launch_seg_softmax_topk(s, logits_dev, probs_dev, top_idx, top_prob, h->seg_dev, h->nseg, B,
+                                    h->C);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            g_err = std::string("head launch failed: ") + hipGetErrorString(e);
+            rc = CLIPVIT_E_HIP;
+        }
+    }
+    release_ws(h, s, w);
+    return rc;
+}
+
+int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype, int B,
+                            int iters, float* out_ms) {
+    g_err.clear();
+    int rc = check_call(h, pixels_dev, dtype, B);
+    if (rc) return rc;
+    if (!out_ms || iters <= 0) FAIL(CLIPVIT_E_INVALID, "bad profile arguments");
+    DeviceGuard dg(h->device);
+    hipStream_t s = (hipStream_t)stream;
+    Workspace* w = nullptr;
+    if ((rc = acquire_ws(h, s, &w))) return rc;
+    Prof p;
+    const size_t nmarks = 8 + 8 * (size_t)h->cfg.layers;
+    p.ev.resize(nmarks);
+    p.fam.resize(nmarks);
+    for (auto& e : p.ev) hipEventCreate(&e);
+    double acc[F_COUNT] = {0};
+    for (int it = 0; it < iters && !rc; ++it) {
+        p.k = 0;
+        rc = forward(h, s, pixels_dev, dtype, B, w, w->f, &p);
+        if (rc) break;
+        hipEventSynchronize(p.ev[p.k - 1]);
+        for (size_t k = 1; k < p.k; ++k) {
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, p.ev[k - 1], p.ev[k]);
+            acc[p.fam[k]] += ms;
+        }
+    }
+    for (auto& e : p.ev) hipEventDestroy(e);
+    release_ws(h, s, w);
+    for (int f = 0; f < F_COUNT; ++f) out_ms[f] = (float)(acc[f] / iters);
+    return rc;
+}
+
+int clipvit_destroy(clipvit_handle* h) {
+    if (!h) return 0;
+    DeviceGuard dg(h->device);
+    hipDeviceSynchronize();
+    for (auto& kv : h->master) hipFree(kv.second);
+    hipFree(h->wpatch);
+    for (auto& ly : h->layers) {
+        hipFree(ly.wqkv);
+        hipFree(ly.wout);
+        hipFree(ly.wfc);
+        hipFree(ly.wproj);
+    }
+    hipFree(h->scratch);
+    hipFree(h->Tt);
+    hipFree(h->seg_dev);
+    for (auto* w : h->pool) free_ws(w);
+    delete h;
+    return 0;
+}
+
+// ---- kernel-level test entry points ----
+int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
+                      const float* bias_dev, float* C_dev, int M, int N, int K, int epi, int variant) {
+    g_err.clear();
+    if (!A_dev || !W_dev || !C_dev) FAIL(CLIPVIT_E_INVALID, "null argument");
+    if (dtype != CLIPVIT_BF16 && dtype != CLIPVIT_F16) FAIL(CLIPVIT_E_INVALID, "dtype");
+    if (K % 64 || N % 64 || M <= 0) FAIL(CLIPVIT_E_INVALID, "K and N must be multiples of 64");
+    hipStream_t s = (hipStream_t)stream;
+    void* Wp = nullptr;
+    HIPCHK(hipMallocAsync(&Wp, (size_t)N * K * 2, s));
+    launch_pack_weight(s, dtype, (const float*)W_dev, Wp, N, K, K);
+    GemmArgs a{};
+    a.A = A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
+    a.M = M; a.N = N; a.K = K; a.ldc = N;
+    const int e = epi == 0 ? EPI_F32 : epi == 1 ? EPI_F32GELU : EPI_RESID;
+    const int rc = launch_gemm(s, dtype, e, a, variant);
+    HIPCHK(hipFreeAsync(Wp, s));
+    if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B, int N,
+                           int H) {
+    g_err.clear();
+    if (!qkv_dev || !out_dev || B <= 0 || N <= 0 || H <= 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
+    launch_attention((hipStream_t)stream, dtype, qkv_dev, out_dev, B, N, H);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

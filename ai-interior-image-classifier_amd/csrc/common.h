@@ -1,0 +1,109 @@
+// Shared device helpers and kernel-launcher declarations for libclipvit_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace clipvit {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+// Element tag types: storage is always 16-bit, T selects the MFMA operand format.
+struct BF16 {
+    typedef bf16x8 vec8;
+    static __device__ __forceinline__ u16 from_f32(float f) {
+        return __builtin_bit_cast(u16, (__bf16)f);
+    }
+    static __device__ __forceinline__ float to_f32(u16 v) {
+        return __builtin_bit_cast(float, (unsigned)v << 16);
+    }
+    static __device__ __forceinline__ f32x4 mfma16(const vec8& a, const vec8& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    }
+};
+struct F16 {
+    typedef f16x8 vec8;
+    static __device__ __forceinline__ u16 from_f32(float f) {
+        return __builtin_bit_cast(u16, (_Float16)f);
+    }
+    static __device__ __forceinline__ float to_f32(u16 v) {
+        return (float)__builtin_bit_cast(_Float16, v);
+    }
+    static __device__ __forceinline__ f32x4 mfma16(const vec8& a, const vec8& b, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+    }
+};
+
+// Pack two fp32 into one dword of two 16-bit values (lo first).
+template <typename T>
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+    return (unsigned)T::from_f32(lo) | ((unsigned)T::from_f32(hi) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// 16-byte async copy global -> LDS (global_load_lds_dwordx4). lds_wave_base must be the
+// wave-uniform LDS destination; lane i lands at lds_wave_base + 16*i.
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((const GLB_AS void*)gsrc, (LDS_AS void*)lds_wave_base, 16, 0,
+                                     0);
+}
+
+// GEMM epilogues.
+enum Epi {
+    EPI_STORE = 0,   // C (T)   = acc + bias
+    EPI_GELU = 1,    // C (T)   = quickgelu(acc + bias)
+    EPI_RESID = 2,   // C (f32) += acc + bias
+    EPI_PATCH = 3,   // C (f32) [remapped token row] = acc          (conv1 has no bias)
+    EPI_F32 = 4,     // C (f32) = acc + bias                         (tests)
+    EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
+};
+
+struct GemmArgs {
+    const void* A;     // [M, K] activations (16-bit), row stride K
+    const void* W;     // [N, K] packed weights (16-bit), row stride K
+    const float* bias; // [N] or nullptr
+    void* C;           // output, row stride ldc (elements)
+    int M, N, K, ldc;
+    int patch_g2, patch_ntok;  // EPI_PATCH row remap: m -> (m / g2) * ntok + 1 + m % g2
+};
+
+// ---- launchers (defined in the .hip translation units) ----
+// variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)
+int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
+
+void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H);
+
+void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, void* acol, int B,
+                   int R, int P, int Kp);
+void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
+                     const float* pos, const float* g_pre, const float* b_pre, const float* g1,
+                     const float* b1, int B, int N, int D);
+void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
+                      const float* b, int rows, int D);
+void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,
+                        int Kp);
+void launch_lora_merge(hipStream_t s, float* W, const float* A, const float* Bm, int in_f,
+                       int out_f, int rank, float scaling);
+void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,
+                        const float* proj, float* f, int B, int N, int D, int E);
+void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_norm, float* logits,
+                   int B, int E, int C, int Cpad);
+void launch_seg_softmax_topk(hipStream_t s, const float* logits, float* probs, int* top_idx,
+                             float* top_prob, const int* seg_off, int nseg, int B, int C);
+
+}  // namespace clipvit

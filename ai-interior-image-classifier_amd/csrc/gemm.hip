@@ -1,0 +1,223 @@
+// MFMA GEMM for every dense contraction of the CLIP ViT encoder (gfx950, wave64).
+//
+//   C[M, N] = A[M, K] @ W[N, K]^T (+ bias) with a fused epilogue
+//
+// A = token activations (row-major, K contiguous), W = nn.Linear weight [out, in] as stored
+// by OpenAI CLIP (attn.in_proj_weight, attn.out_proj.weight, mlp.c_fc.weight,
+// mlp.c_proj.weight; conv1.weight viewed as [width, 3*p*p]).  Both operands are K-major, so
+// every MFMA fragment is one 16-byte LDS read.
+//
+// Design:
+//  * block tile BM x BN x 64, waves arranged WM x WN, each wave TM x TN = (BM/WM) x (BN/WN);
+//  * global -> LDS by global_load_lds_dwordx4 (no VGPR staging), two LDS buffers, next tile's
+//    loads issued before the current tile's MFMAs;
+//  * LDS rows are 128 B (64 x 16-bit); 16-B chunk c of row r lives at chunk c ^ (r & 7) — the
+//    swizzle is applied to the per-lane global SOURCE address (glds writes lane-linearly) and to
+//    the ds_read address, which makes every ds_read_b128 wave-instruction conflict-free;
+//  * swapped operands: MFMA A-operand = weight rows, B-operand = token rows, so the 16x16
+//    accumulator holds C^T: lane (j = lane&15, g = lane>>4) owns token j and 4 features.
+//    W is packed with its rows permuted inside every 64-row group (launch_pack_weight) so that
+//    over four consecutive 16-row subtiles a lane owns 16 CONTIGUOUS output features -> 32-B
+//    (16-bit) or 64-B (fp32) vector stores in the epilogue, no shuffles;
+//  * v_mfma_f32_16x16x32_{bf16,f16}, fp32 accumulation; epilogue adds bias, QuickGELU
+//    (x * sigmoid(1.702 x), CLIP's activation) or the fp32 residual add;
+//  * bijective XCD-aware block remap: consecutive logical tiles (same A panel) share an XCD L2.
+#include "common.h"
+
+namespace clipvit {
+
+template <typename T, int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM* WN) void gemm_nt_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(TN % 64 == 0, "wave N-tile must be a multiple of 64 (packed groups)");
+    static_assert(TM % 16 == 0, "wave M-tile must be a multiple of 16");
+    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
+    static_assert(A_BYTES % (NT * 16) == 0 && W_BYTES % (NT * 16) == 0, "staging rounds");
+    constexpr int STAGE = A_BYTES + W_BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+
+    const int nN = a.N / BN;
+    const int nwg = gridDim.x;
+    int bid = blockIdx.x;
+    {  // bijective XCD remap: blocks b, b+8, ... (one XCD) take a contiguous logical range
+        const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
+
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K * 2;  // row stride in bytes (A and W)
+    const int mlast = a.M - 1;
+
+    auto stage = [&](int buf, int kt) {
+        unsigned char* sA = smem + buf * STAGE;
+        unsigned char* sW = sA + A_BYTES;
+        const size_t kofs = (size_t)kt * 128;
+#pragma unroll
+        for (int r = 0; r < A_BYTES / (NT * 16); ++r) {
+            const int p = r * NT * 16 + tid * 16;
+            const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
+            const int grow = min(m0 + row, mlast);
+            glds16(Ab + (size_t)grow * ldb + kofs + c * 16, sA + r * NT * 16 + wave * 1024);
+        }
+#pragma unroll
+        for (int r = 0; r < W_BYTES / (NT * 16); ++r) {
+            const int p = r * NT * 16 + tid * 16;
+            const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
+            glds16(Wb + (size_t)(n0 + row) * ldb + kofs + c * 16, sW + r * NT * 16 + wave * 1024);
+        }
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = a.K >> 6;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const int lrow = lane & 15, lsw = lane & 7;
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+        const unsigned char* sA = smem + cur * STAGE;
+        const unsigned char* sW = sA + A_BYTES;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = ((s << 2) | (lane >> 4)) ^ lsw;
+            vec8 af[FM], wf[FN];
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+                af[fm] = *(const vec8*)(sA + (wm * TM + fm * 16 + lrow) * 128 + (c << 4));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+                wf[fn] = *(const vec8*)(sW + (wn * TN + fn * 16 + lrow) * 128 + (c << 4));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane owns token m and features n .. n+15 of each 64-feature group ----
+    const int g = lane >> 4;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = m0 + wm * TM + fm * 16 + lrow;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int q = 0; q < FN / 4; ++q) {
+            const int n = n0 + wn * TN + q * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
+            if constexpr (EPI != EPI_PATCH) {
+                if (a.bias) {
+                    const float4* b4 = (const float4*)(a.bias + n);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 bb = b4[i];
+                        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                    }
+                }
+            }
+            if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+            }
+            if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+                dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                    pack2<T>(v[6], v[7]));
+                dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                    pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+            } else if constexpr (EPI == EPI_RESID) {
+                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float4 o = dst[i];
+                    o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                    dst[i] = o;
+                }
+            } else {
+                size_t row = (size_t)m;
+                if constexpr (EPI == EPI_PATCH)
+                    row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
+                float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        }
+    }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+static void launch_tile(hipStream_t s, int epi, const GemmArgs& a) {
+    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+    dim3 grid(nwg), block(64 * WM * WN);
+    switch (epi) {
+        case EPI_STORE: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+        case EPI_PATCH: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+    }
+}
+
+// Auto tile choice: the largest tile whose grid still covers the 256 CUs reasonably.
+static int pick_variant(const GemmArgs& a) {
+    const long t256 = (long)(a.N % 256 == 0 ? a.N / 256 : 0) * ((a.M + 255) / 256);
+    const long t256x128 = (long)(a.N / 128) * ((a.M + 255) / 256);
+    if (t256 >= 400) return 3;
+    if (a.N % 128 == 0 && t256x128 >= 400) return 2;
+    return 1;
+}
+
+template <typename T>
+static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
+    if (variant == 0) variant = pick_variant(a);
+    switch (variant) {
+        case 1:
+            if (a.N % 128) return -1;
+            launch_tile<T, 128, 128, 2, 2>(s, epi, a);
+            return 0;
+        case 2:
+            if (a.N % 128) return -1;
+            launch_tile<T, 256, 128, 4, 2>(s, epi, a);
+            return 0;
+        case 3:
+            if (a.N % 256) return -1;
+            launch_tile<T, 256, 256, 2, 4>(s, epi, a);
+            return 0;
+        case 4:
+            if (a.N % 64) return -1;
+            launch_tile<T, 64, 64, 4, 1>(s, epi, a);
+            return 0;
+    }
+    return -1;
+}
+
+int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
+    if (a.K % 64 != 0 || a.M <= 0) return -1;
+    if (dtype == 2) return launch_t<F16>(s, epi, a, variant);
+    return launch_t<BF16>(s, epi, a, variant);
+}
+
+}  // namespace clipvit

@@ -1,0 +1,252 @@
+// Memory-bound kernels of the encoder: patch im2col, token assembly + ln_pre + ln_1,
+// LayerNorm, weight packing and the load-time LoRA merge.
+//
+// Reference semantics (OpenAI-CLIP VisionTransformer.forward [3p], called via
+// model.encode_image at main.py:204 / 444 / 503):
+//   x = conv1(pixels)                         (no bias; -> im2col + MFMA GEMM, EPI_PATCH)
+//   x = cat([class_embedding, x]) + positional_embedding
+//   x = ln_pre(x)                             (CLIP LayerNorm: computed in fp32, eps 1e-5)
+//   per block: x = x + attn(ln_1(x)); x = x + mlp(ln_2(x))
+// LoRA (main.py:19-31): y = x W^T + b + (x A B) * (alpha / r)  ==  x (W + s (A B)^T)^T + b.
+#include "common.h"
+
+namespace clipvit {
+
+// ---------------------------------------------------------------------------------------
+// im2col of non-overlapping p x p patches: acol[b*G*G + py*G + px][c*p*p + i*p + j]
+//   = pix[b][c][py*p + i][px*p + j], columns >= 3*p*p zero-padded up to Kp (multiple of 64).
+// One thread writes 8 consecutive columns (one 16-byte store).
+template <int IN>
+__device__ __forceinline__ float load_pix(const void* p, size_t off) {
+    if constexpr (IN == 0) return ((const float*)p)[off];
+    else if constexpr (IN == 1) return BF16::to_f32(((const u16*)p)[off]);
+    else return F16::to_f32(((const u16*)p)[off]);
+}
+
+template <typename TO, int IN>
+__global__ void im2col_kernel(const void* __restrict__ pix, u16* __restrict__ acol, int B, int R,
+                              int P, int Kp) {
+    const int G = R / P, G2 = G * G, K3 = 3 * P * P;
+    const long total = (long)B * G2 * (Kp / 8);
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int kc = (int)(idx % (Kp / 8));
+    const long row = idx / (Kp / 8);
+    const int b = (int)(row / G2), pp = (int)(row % G2);
+    const int py = pp / G, px = pp % G;
+    float v[8];
+    const int k0 = kc * 8;
+    if (k0 + 8 <= K3 && (P % 8) == 0) {
+        // 8 consecutive columns = 8 consecutive pixels of one patch row
+        const int c = k0 / (P * P), rem = k0 % (P * P), i = rem / P, jj = rem % P;
+        const size_t off = (((size_t)b * 3 + c) * R + (py * P + i)) * R + px * P + jj;
+        if constexpr (IN == 0) {
+            const float4* src = (const float4*)((const float*)pix + off);
+            const float4 a0 = src[0], a1 = src[1];
+            v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
+            v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+        } else {
+            const uint4 w = *(const uint4*)((const u16*)pix + off);
+            const u16* hv = (const u16*)&w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                v[e] = IN == 1 ? BF16::to_f32(hv[e]) : F16::to_f32(hv[e]);
+        }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = k0 + e;
+            float val = 0.f;
+            if (k < K3) {
+                const int c = k / (P * P), rem = k % (P * P), i = rem / P, jj = rem % P;
+                val = load_pix<IN>(pix, (((size_t)b * 3 + c) * R + (py * P + i)) * R + px * P + jj);
+            }
+            v[e] = val;
+        }
+    }
+    uint4 o = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                         pack2<TO>(v[6], v[7]));
+    *(uint4*)(acol + row * Kp + k0) = o;
+}
+
+template <typename TO>
+static void im2col_dispatch(hipStream_t s, int in_dtype, const void* pix, void* acol, int B, int R,
+                            int P, int Kp) {
+    const int G = R / P;
+    const long total = (long)B * G * G * (Kp / 8);
+    const int threads = 256;
+    const long blocks = (total + threads - 1) / threads;
+    if (in_dtype == 0) im2col_kernel<TO, 0><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
+    else if (in_dtype == 1) im2col_kernel<TO, 1><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
+    else im2col_kernel<TO, 2><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
+}
+
+void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, void* acol, int B,
+                   int R, int P, int Kp) {
+    if (out_dtype == 2) im2col_dispatch<F16>(s, in_dtype, pix, acol, B, R, P, Kp);
+    else im2col_dispatch<BF16>(s, in_dtype, pix, acol, B, R, P, Kp);
+}
+
+// ---------------------------------------------------------------------------------------
+// Row LayerNorm helpers: one wave per row, D = 64 * 4 * V (V float4 per lane).
+template <int V>
+__device__ __forceinline__ void ln_row(float4 (&v)[V], const float* __restrict__ gm,
+                                       const float* __restrict__ bt, int lane, float D) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mean = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+    }
+    const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        const float4 gg = *(const float4*)(gm + c), bb = *(const float4*)(bt + c);
+        v[i].x = v[i].x * rstd * gg.x + bb.x;
+        v[i].y = v[i].y * rstd * gg.y + bb.y;
+        v[i].z = v[i].z * rstd * gg.z + bb.z;
+        v[i].w = v[i].w * rstd * gg.w + bb.w;
+    }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int lane) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        *(uint2*)(dst + c) = make_uint2(pack2<T>(v[i].x, v[i].y), pack2<T>(v[i].z, v[i].w));
+    }
+}
+
+// x[row] = ln_pre((t == 0 ? class_embedding : patch_row) + pos[t]);  h[row] = ln_1(x[row])
+template <typename T, int V>
+__global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, u16* __restrict__ h,
+                                                       const float* __restrict__ cls,
+                                                       const float* __restrict__ pos,
+                                                       const float* __restrict__ gp,
+                                                       const float* __restrict__ bp,
+                                                       const float* __restrict__ g1,
+                                                       const float* __restrict__ b1, int rows,
+                                                       int N) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int t = row % N;
+    constexpr int D = 256 * V;
+    float* xr = x + (size_t)row * D;
+    const float* src = t == 0 ? cls : xr;
+    const float* pr = pos + (size_t)t * D;
+    float4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        const float4 a = *(const float4*)(src + c), p = *(const float4*)(pr + c);
+        v[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+    }
+    ln_row<V>(v, gp, bp, lane, (float)D);
+#pragma unroll
+    for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    ln_row<V>(v, g1, b1, lane, (float)D);
+    store_row16<T, V>(h + (size_t)row * D, v, lane);
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x,
+                                                        u16* __restrict__ h,
+                                                        const float* __restrict__ gm,
+                                                        const float* __restrict__ bt, int rows) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    constexpr int D = 256 * V;
+    const float* xr = x + (size_t)row * D;
+    float4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
+    ln_row<V>(v, gm, bt, lane, (float)D);
+    store_row16<T, V>(h + (size_t)row * D, v, lane);
+}
+
+#define DISPATCH_V(D, ...)                          \
+    switch ((D) / 256) {                            \
+        case 2: { constexpr int V = 2; __VA_ARGS__; } break; \
+        case 3: { constexpr int V = 3; __VA_ARGS__; } break; \
+        case 4: { constexpr int V = 4; __VA_ARGS__; } break; \
+        case 5: { constexpr int V = 5; __VA_ARGS__; } break; \
+        default: break;                             \
+    }
+
+void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
+                     const float* pos, const float* g_pre, const float* b_pre, const float* g1,
+                     const float* b1, int B, int N, int D) {
+    const int rows = B * N;
+    dim3 grid((rows + 3) / 4), block(256);
+    if (dtype == 2) {
+        DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)h, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+    } else {
+        DISPATCH_V(D, embed_ln_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)h, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+    }
+}
+
+void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
+                      const float* b, int rows, int D) {
+    dim3 grid((rows + 3) / 4), block(256);
+    if (dtype == 2) {
+        DISPATCH_V(D, layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)h, g, b, rows));
+    } else {
+        DISPATCH_V(D, layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)h, g, b, rows));
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Pack an fp32 [N, K] Linear weight into the GEMM's operand layout: 16-bit, K padded to Kp,
+// rows permuted inside each 64-row group so that packed row p = 16 f + i holds original row
+// 16 (i >> 2) + 4 f + (i & 3)  (see gemm.hip: the swapped-operand epilogue then owns 16
+// contiguous output features per lane).
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ src, u16* __restrict__ dst, int N,
+                                   int K, int Kp) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)N * Kp) return;
+    const int p = (int)(idx / Kp), k = (int)(idx % Kp);
+    const int grp = p & ~63, pi = p & 63, f = pi >> 4, i = pi & 15;
+    const int n = grp + 16 * (i >> 2) + 4 * f + (i & 3);
+    const float v = k < K ? src[(size_t)n * K + k] : 0.f;
+    dst[idx] = T::from_f32(v);
+}
+
+void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,
+                        int Kp) {
+    const long total = (long)N * Kp;
+    const int threads = 256;
+    const long blocks = (total + threads - 1) / threads;
+    if (dtype == 2) pack_weight_kernel<F16><<<blocks, threads, 0, s>>>(src, (u16*)dst, N, K, Kp);
+    else pack_weight_kernel<BF16><<<blocks, threads, 0, s>>>(src, (u16*)dst, N, K, Kp);
+}
+
+// W[o][i] += scaling * sum_r A[i][r] * B[r][o]   (fp32, once at load time)
+__global__ void lora_merge_kernel(float* __restrict__ W, const float* __restrict__ A,
+                                  const float* __restrict__ Bm, int in_f, int out_f, int rank,
+                                  float scaling) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (long)in_f * out_f) return;
+    const int o = (int)(idx / in_f), i = (int)(idx % in_f);
+    float acc = 0.f;
+    for (int r = 0; r < rank; ++r) acc += A[(size_t)i * rank + r] * Bm[(size_t)r * out_f + o];
+    W[idx] += scaling * acc;
+}
+
+void launch_lora_merge(hipStream_t s, float* W, const float* A, const float* Bm, int in_f,
+                       int out_f, int rank, float scaling) {
+    const long total = (long)in_f * out_f;
+    const int threads = 256;
+    lora_merge_kernel<<<(total + threads - 1) / threads, threads, 0, s>>>(W, A, Bm, in_f, out_f,
+                                                                         rank, scaling);
+}
+
+}  // namespace clipvit

@@ -1,0 +1,190 @@
+"""Benchmark of the MI355X CLIP-ViT image path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one ``classify`` of a resident synthetic batch (ViT-B/32 + merged LoRA r=8, bf16 MFMA,
+224x224, 256 images per GPU): patch-embed -> 12 blocks -> ln_post/proj -> L2-norm -> 100*cos
+logits over 437 labels -> segment softmax + top-5, followed (N > 1) by the RCCL all-gather of
+the per-image logits. Rank 0 prints ONE JSON line. Per-GPU work is fixed as N grows
+(scaling = "weak"); value = images/s of the whole job = N * 256 * K / max-over-ranks time.
+
+Extra objects on the line:
+  roofline     dominant kernel family (MLP GEMMs c_fc + c_proj), algorithmic FLOP per launch /
+               average launch time measured with HIP events on the launch stream; peak = dense
+               bf16 MFMA 2.5166 PF/s (MI355X_MICROARCH.md); traffic = PMC HBM bytes per launch
+               from profiles/ (null until measured);
+  cpu_baseline the CPU fp32 oracle restatement of the same forward (port), timed on the host
+               cores on a bounded sample (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import amd_pkg  # noqa: E402
+
+amd_pkg.load()
+from interior_amd import config as C  # noqa: E402
+from interior_amd.dp import allgather_rows, env_rank  # noqa: E402
+from interior_amd.engine import VisionEngine  # noqa: E402
+from interior_amd.lora import synthetic_adapters  # noqa: E402
+from interior_amd.weights import synthetic_state_dict  # noqa: E402
+
+PEAK_TFLOPS = {"bf16": 2516.6, "fp16": 2516.6}
+N_CLASSES = 437
+SEGMENTS = [0, 40, 60, 359, 395, 425, 437]  # detector | styles | characteristics | materials | colors | room types
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--model", default="ViT-B/32")
+    p.add_argument("--batch", type=int, default=256, help="images per GPU")
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp16"])
+    p.add_argument("--lora-rank", type=int, default=8)
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-iters", type=int, default=5)
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds: float):
+    """The oracle (CPU fp32 restatement, 'port') on the host cores: bs=16 (reference default,
+    main.py:592) batches of the same synthetic inputs until ~`seconds` of work."""
+    from oracle import clip_ref
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    sd = synthetic_state_dict(cfg, 0)
+    geo = clip_ref.GEOMETRIES[cfg.name]
+    g = torch.Generator().manual_seed(0)
+    px = torch.randn(16, 3, cfg.image_size, cfg.image_size, generator=g).clamp_(-1.8, 2.2)
+    T = torch.nn.functional.normalize(torch.randn(N_CLASSES, cfg.embed_dim, generator=g), dim=-1)
+    with torch.no_grad():
+        clip_ref.head(clip_ref.encode_image(sd, geo, px[:2]), T, SEGMENTS)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            clip_ref.head(clip_ref.encode_image(sd, geo, px), T, SEGMENTS)
+            n += px.shape[0]
+            el = time.perf_counter() - t0
+            if el >= seconds and n >= 32:
+                break
+    return {"value": round(n / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} synthetic {cfg.image_size}px images, bs=16, {cfg.name} fp32 torch-CPU oracle "
+                      f"(encode + head), {el:.1f}s"}
+
+
+def load_traffic(cfg_name: str, batch: int):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        e = d.get(f"{cfg_name}|{batch}")
+        return None if e is None else e.get("mlp_gemm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    rank, local_rank, world = env_rank()
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    cfg = C.get_config(a.model)
+
+    eng = VisionEngine(cfg, dev, a.dtype, max_batch=a.batch)
+    eng.load_state_dict(synthetic_state_dict(cfg, 0))
+    if a.lora_rank:
+        eng.load_lora(synthetic_adapters(cfg, rank=a.lora_rank))
+    g = torch.Generator().manual_seed(1234)
+    T = torch.nn.functional.normalize(torch.randn(N_CLASSES, cfg.embed_dim, generator=g), dim=-1)
+    eng.set_text_features(T.numpy(), SEGMENTS)
+    gpx = torch.Generator(device=dev).manual_seed(100 + rank)
+    px = torch.randn(a.batch, 3, cfg.image_size, cfg.image_size, device=dev, generator=gpx).clamp_(-1.8, 2.2)
+    out = eng.classify(px)   # allocates the output buffers once
+
+    def step():
+        eng.classify(px, out)
+        if world > 1:
+            allgather_rows(out.logits)
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    imgs = world * a.batch * a.steps
+    value = imgs / el
+
+    # live per-kernel-family device times (HIP events on the launch stream)
+    fam = eng.profile_forward(px, iters=a.profile_iters)
+    D, N, M = cfg.width, cfg.tokens, a.batch * cfg.tokens
+    mlp_flop = 2.0 * M * D * 4 * D  # c_fc and c_proj each
+    mlp_ms = (fam["fc_gemm"] + fam["proj_gemm"]) / (2 * cfg.layers)  # per launch
+    achieved = mlp_flop / (mlp_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[a.dtype]
+    model_tflops = value / world * cfg.gflop_per_image() / 1e3
+
+    line = {
+        "metric": "images/sec @ 224x224 bs=256, ViT-B/32+LoRA, 1/2/4/8 MI355X; % MFMA roofline",
+        "value": round(value, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(el / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": a.dtype,
+        "data": "synthetic (seeded N(0,1) pixels clamped to CLIP-normalised range, seeded CLIP-style weights, synthetic unit text features)",
+        "config": {"workload": f"{cfg.name} + merged LoRA r={a.lora_rank} classify (encode_image + cosine head over {N_CLASSES} labels, 6 segments)",
+                   "image_size": cfg.image_size, "per_gpu_batch": a.batch, "global_batch": a.batch * world,
+                   "parallelism": f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else "")},
+        "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj+residual)",
+                     "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),
+                     "flop_per_launch": mlp_flop, "avg_launch_ms": round(mlp_ms, 5),
+                     "model_mfma_frac": round(model_tflops / peak, 4),
+                     "family_ms_per_forward": {k: round(v, 4) for k, v in fam.items()}},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,166 @@
+/*
+ * clipvit.h — C ABI of libclipvit_hip.so, the MI355X (gfx950) CLIP-ViT image path.
+ *
+ * This library replaces, for the hot path only, the `(model, preprocess)` pair that the
+ * reference obtains from `clip.load("ViT-B/16", device)` (main.py:152, main.py:241,
+ * python-worker/main_API.py:137) and the cosine head that main.py computes around it.
+ * Each entry point names the reference interface it stands in for.
+ *
+ * Conventions
+ *   - every function returns int status: 0 = OK, negative = error; the message of the
+ *     last error on the calling host thread is returned by clipvit_last_error().
+ *   - "dev" pointers are device (HBM) pointers on the handle's device, owned by the caller.
+ *   - a handle is pinned to one device; weights are immutable after loading, so
+ *     encode/classify may be called concurrently from several host threads (each call
+ *     takes a workspace from a mutex-guarded pool, ordered by HIP events).
+ *   - stream arguments are hipStream_t passed as void*; NULL = the legacy default stream.
+ *   - no torch types cross this boundary: plain pointers, sizes and enums only.
+ */
+#ifndef CLIPVIT_H
+#define CLIPVIT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLIPVIT_ABI_VERSION 1
+
+/* Status codes. */
+#define CLIPVIT_OK 0
+#define CLIPVIT_E_INVALID (-1)   /* bad argument / shape / name                         */
+#define CLIPVIT_E_HIP (-2)       /* a HIP runtime call failed                           */
+#define CLIPVIT_E_STATE (-3)     /* call out of order (e.g. classify before text feats) */
+#define CLIPVIT_E_NOMEM (-4)     /* device allocation failed                             */
+
+/* Element types of buffers crossing the ABI. */
+typedef enum {
+    CLIPVIT_F32 = 0,
+    CLIPVIT_BF16 = 1,
+    CLIPVIT_F16 = 2,
+} clipvit_dtype;
+
+/* Model geometry. Mirrors OpenAI-CLIP VisionTransformer(input_resolution, patch_size,
+ * width, layers, heads, output_dim) as built by clip.load [3p] for the name passed at
+ * main.py:152 / main.py:241.  compute_dtype selects the MFMA operand type (BF16 or F16);
+ * the residual stream, LayerNorm statistics, softmax and the head stay fp32. */
+typedef struct {
+    int image_size;     /* 224 (B/32, B/16) or 336 (L/14@336)          */
+    int patch_size;     /* 32, 16, 14                                   */
+    int width;          /* 768 / 1024  (multiple of 256)                */
+    int layers;         /* 12 / 24                                      */
+    int heads;          /* width / 64                                   */
+    int embed_dim;      /* 512 / 768   (multiple of 64)                 */
+    int compute_dtype;  /* CLIPVIT_BF16 or CLIPVIT_F16                  */
+    int max_batch;      /* largest B accepted by encode/classify        */
+} clipvit_config;
+
+/* A host fp32 tensor keyed by its OpenAI-CLIP state-dict name (e.g.
+ * "visual.transformer.resblocks.3.mlp.c_fc.weight"). Row-major, contiguous. */
+typedef struct {
+    const char* name;
+    const float* data;
+    int ndim;
+    int64_t shape[4];
+} clipvit_tensor;
+
+/* One LoRA adapter to merge into a Linear of the vision tower.
+ * Reference layout (main.py:19-31): lora_A [in, rank], lora_B [rank, out],
+ * forward = linear(x) + (x @ A @ B) * scaling  with scaling = alpha / rank.
+ * target = OpenAI name of the Linear's weight, e.g.
+ * "visual.transformer.resblocks.0.attn.in_proj_weight" or "...mlp.c_fc.weight". */
+typedef struct {
+    const char* target;
+    const float* A;   /* [in, rank]  host fp32 */
+    const float* B;   /* [rank, out] host fp32 */
+    int in_features;
+    int out_features;
+    int rank;
+    float scaling;    /* alpha / rank */
+} clipvit_lora;
+
+typedef struct clipvit_handle clipvit_handle;
+
+/* Replaces clip.load(name, device) model construction (main.py:152, main.py:241).
+ * Allocates the weight store and the first workspace for cfg->max_batch images. */
+int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
+
+/* Replaces the weight half of clip.load [3p]: host fp32 tensors keyed by OpenAI names.
+ * The library copies them to HBM, keeps fp32 masters, and packs the MFMA operands.
+ * Every visual.* tensor of the geometry must be present (text-tower names are ignored). */
+int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_t n);
+
+/* Replaces replace_linears_with_lora + load_lora_weights_to_model (main.py:62-113) for the
+ * vision tower: W' = W + scaling * (A @ B)^T merged into the fp32 master, then re-packed.
+ * Linears with no adapter keep a zero delta (lora_B = 0 init, main.py:27). Runtime cost 0. */
+int clipvit_load_lora(clipvit_handle* h, const clipvit_lora* items, size_t n);
+
+/* Replaces the cached text matrices of InteriorImageDetector (main.py:179-182) and
+ * CachedInteriorAnalyzer._precompute_text_features_optimized (main.py:296-311):
+ * T [C, E] host fp32 rows (already L2-normalised by the caller, as the reference does),
+ * split into nseg consecutive segments by seg_offsets[0..nseg] (seg_offsets[0] = 0,
+ * seg_offsets[nseg] = C). Softmax and top-k run independently per segment. */
+int clipvit_set_text_features(clipvit_handle* h, const float* T, int C, int E,
+                              const int* seg_offsets, int nseg);
+
+/* Replaces model.encode_image(x) (main.py:204, main.py:444, main.py:503).
+ * pixels_dev: [B, 3, R, R] CLIP-normalised pixels of `dtype`; emb_dev: [B, E] fp32,
+ * the projected image features BEFORE L2 normalisation (what encode_image returns). */
+int clipvit_encode_image(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype,
+                         int B, float* emb_dev);
+
+/* Replaces encode_image + the head of main.py:205-217 / 445-459 / 504-509:
+ *   f = encode_image(x); f /= ||f||; logits = 100 * f @ T^T; per segment softmax + topk(min(5,n)).
+ * Outputs (any may be NULL except logits):
+ *   emb_dev    [B, E]      fp32, L2-normalised features
+ *   logits_dev [B, C]      fp32
+ *   probs_dev  [B, C]      fp32, softmax within each segment
+ *   top_idx    [B, nseg, 5] int32 column index inside the segment (-1 where n < 5)
+ *   top_prob   [B, nseg, 5] fp32 */
+int clipvit_classify(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype, int B,
+                     float* emb_dev, float* logits_dev, float* probs_dev, int32_t* top_idx,
+                     float* top_prob);
+
+/* Number of text classes / segments currently set (0 if none). */
+int clipvit_text_shape(clipvit_handle* h, int* C, int* nseg);
+
+/* Frees every device allocation of the handle. */
+int clipvit_destroy(clipvit_handle* h);
+
+/* Thread-local message of the last failing call on this host thread ("" if none). */
+const char* clipvit_last_error(void);
+
+/* ABI version compiled into the library (CLIPVIT_ABI_VERSION). */
+int clipvit_abi_version(void);
+
+/* ---- kernel-level entry points (testing / benchmarking of single hot kernels) ----
+ * These operate on caller-owned device buffers with the packed layouts documented in
+ * DESIGN.md; they are what the per-kernel parity tests and the roofline probe call. */
+
+/* C[M,N] = A[M,K] @ W[N,K]^T + bias.  A_dev: 16-bit (`dtype` BF16/F16) row-major;
+ * W_dev: fp32 [N,K] natural row order (packed to `dtype` internally, as clipvit_load_weights
+ * does); bias fp32 [N] or NULL; C fp32 [M,N]. epi: 0 = store, 1 = QuickGELU then store,
+ * 2 = accumulate into C (residual add). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
+ * N % 256 for variant 3). variant: 0 auto, 1 128x128, 2 256x128, 3 256x256, 4 64x64. */
+int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
+                      const float* bias_dev, float* C_dev, int M, int N, int K, int epi,
+                      int variant);
+
+/* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
+ * out [B*N, H*64] of `dtype`. */
+int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B,
+                           int N, int H);
+
+/* Time `iters` launches of the encoder forward at batch B on `stream`; returns the
+ * average per-kernel-family device time (ms) into out_ms[0..7]:
+ * 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm, 5 fc gemm,
+ * 6 proj gemm, 7 head. Requires weights loaded. Used by bench.py's roofline probe. */
+int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype,
+                            int B, int iters, float* out_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLIPVIT_H */

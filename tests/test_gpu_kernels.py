@@ -1,0 +1,102 @@
+"""Per-kernel parity on the GPU, through the C ABI test entry points.
+
+GEMM: fp32 torch reference of the same op on the 16-bit-rounded operands (tolerance from
+fp32-accumulation order only: 2e-3 relative to max|C|). Attention: the oracle's fp32
+attention on the same 16-bit q/k/v; P is rounded to 16 bit before P.V (flash-style), so the
+bound is 1e-2 of max|O| for bf16 and 3e-3 for fp16.
+"""
+import math
+
+import pytest
+import torch
+
+from interior_amd import engine as E
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_gemm(A, W, bias, epi, C0=None):
+    ref = A.float() @ W.to(A.dtype).float().t()
+    if bias is not None:
+        ref = ref + bias
+    if epi == 1:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    if epi == 2:
+        ref = ref + C0
+    return ref
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
+                                   (700, 768, 3072), (64, 256, 64)])
+def test_gemm_shapes(gpu, dtype, variant, M, N, K):
+    if variant in (1, 2) and N % 128 or variant == 3 and N % 256:
+        pytest.skip("tile does not divide N")
+    g = torch.Generator(device=gpu).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(N, device=gpu, generator=g)
+    C = E.gemm_test(A, W, bias, epi=0, variant=variant)
+    ref = _ref_gemm(A, W, bias, 0)
+    err = (C - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-3, err
+
+
+@pytest.mark.parametrize("epi", [0, 1, 2])
+def test_gemm_epilogues(gpu, epi):
+    dtype = torch.bfloat16
+    M, N, K = 515, 1024, 512
+    g = torch.Generator(device=gpu).manual_seed(7)
+    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(N, device=gpu, generator=g)
+    C0 = torch.randn(M, N, device=gpu, generator=g)
+    C = E.gemm_test(A, W, bias, epi=epi, variant=0, C=C0.clone())
+    ref = _ref_gemm(A, W, bias, epi, C0)
+    err = (C - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-3, err
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I, asymmetric W: catches any row/column or permutation mix-up in the epilogue."""
+    K = N = 256
+    A = torch.eye(K, device=gpu).to(torch.bfloat16)
+    W = (torch.arange(N * K, device=gpu, dtype=torch.float32).reshape(N, K) % 251) / 8.0
+    for variant in (1, 2, 3, 4):
+        C = E.gemm_test(A, W, None, epi=0, variant=variant)
+        assert torch.equal(C, W.to(torch.bfloat16).float().t()), variant
+
+
+def _ref_attention(qkv, B, N, H):
+    D = H * 64
+    x = qkv.float().reshape(B, N, 3, H, 64)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(64)
+    o = s.softmax(-1) @ v
+    return o.transpose(1, 2).reshape(B * N, D)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2), (torch.float16, 3e-3)])
+@pytest.mark.parametrize("B,N,H", [(3, 50, 12), (2, 197, 12), (1, 577, 16), (2, 1, 12), (1, 65, 12)])
+def test_attention(gpu, dtype, tol, B, N, H):
+    g = torch.Generator(device=gpu).manual_seed(B * N * H)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).to(dtype)
+    out = E.attention_test(qkv, B, N, H)
+    ref = _ref_attention(qkv, B, N, H)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < tol, err
+
+
+def test_attention_spiky_scores(gpu):
+    """A key far above the rest of its block forces the online-softmax rescale across
+    key blocks (N = 197 -> 4 key blocks): the late block's max must rescale earlier blocks."""
+    B, N, H = 1, 197, 12
+    g = torch.Generator(device=gpu).manual_seed(3)
+    qkv = torch.randn(B * N, 3 * H * 64, device=gpu, generator=g)
+    qkv[150, H * 64: 2 * H * 64] *= 6.0   # one large key in the third block
+    qkv = qkv.to(torch.float16)
+    out = E.attention_test(qkv, B, N, H)
+    ref = _ref_attention(qkv, B, N, H)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 3e-3, err

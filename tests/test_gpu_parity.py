@@ -1,0 +1,129 @@
+"""End-to-end parity of the HIP encoder + head against the CPU fp32 oracle.
+
+Bar: per image max|Δlogit| / max|logit_ref| <= 1e-3 and identical
+per-segment argmax labels, where the margin between the oracle's top-1 and top-2 exceeds the
+measured error (near-ties are reported, not asserted). Embeddings: cosine(f_gpu, f_ref).
+"""
+import numpy as np
+import pytest
+import torch
+
+from interior_amd import config as C
+from interior_amd.engine import VisionEngine
+from interior_amd.lora import synthetic_adapters
+from interior_amd.weights import synthetic_state_dict
+from oracle import clip_ref
+
+pytestmark = pytest.mark.gpu
+
+LOGIT_TOL = {"bf16": 1e-3, "fp16": 1e-3}
+
+
+def _pixels(B, R, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(B, 3, R, R, generator=g).clamp_(-1.8, 2.2)
+
+
+def _text(E, C_, seed=5):
+    g = torch.Generator().manual_seed(seed)
+    T = torch.randn(C_, E, generator=g)
+    return T / T.norm(dim=-1, keepdim=True)
+
+
+def _merged(sd, adapters):
+    out = dict(sd)
+    for a in adapters:
+        out[a.target] = clip_ref.merge_lora(sd[a.target], torch.from_numpy(a.A), torch.from_numpy(a.B),
+                                            a.scaling)
+    return out
+
+
+_ENGINES = {}
+
+
+def _engine(cfg, dtype, lora_rank=0, max_batch=256):
+    key = (cfg.name, dtype, lora_rank, max_batch)
+    if key not in _ENGINES:
+        sd = synthetic_state_dict(cfg, 0)
+        eng = VisionEngine(cfg, 0, dtype, max_batch)
+        eng.load_state_dict(sd)
+        ref_sd = sd
+        if lora_rank:
+            ad = synthetic_adapters(cfg, rank=lora_rank)
+            eng.load_lora(ad)
+            ref_sd = _merged(sd, ad)
+        _ENGINES[key] = (eng, ref_sd)
+    return _ENGINES[key]
+
+
+def _check_logits(lg, lr, seg, tol):
+    rel = (np.abs(lg - lr).max(axis=1) / np.abs(lr).max(axis=1))
+    assert rel.max() <= tol, f"max rel logit err {rel.max():.2e} > {tol}"
+    bad = []
+    for s in range(len(seg) - 1):
+        a, b = seg[s], seg[s + 1]
+        top_r = lr[:, a:b].argmax(1)
+        top_g = lg[:, a:b].argmax(1)
+        srt = np.sort(lr[:, a:b], axis=1)
+        margin = srt[:, -1] - srt[:, -2] if b - a > 1 else np.full(len(lr), np.inf)
+        err = np.abs(lg - lr)[:, a:b].max(1)
+        decided = margin > 2 * err
+        bad += [(i, s) for i in np.nonzero(decided & (top_r != top_g))[0]]
+    assert not bad, f"argmax differs on decided rows: {bad[:5]}"
+    return rel.max()
+
+
+@pytest.mark.parametrize("name,dtype,B,lora", [
+    ("ViT-B/32", "bf16", 8, 0),
+    ("ViT-B/32", "bf16", 8, 8),
+    ("ViT-B/32", "fp16", 8, 8),
+    ("ViT-B/16", "bf16", 4, 0),
+    ("ViT-B/16", "fp16", 4, 4),
+    ("ViT-L/14@336px", "fp16", 2, 16),
+])
+def test_classify_matches_oracle(gpu, name, dtype, B, lora):
+    cfg = C.get_config(name)
+    eng, ref_sd = _engine(cfg, dtype, lora, max_batch=16)
+    px = _pixels(B, cfg.image_size, seed=11)
+    T = _text(cfg.embed_dim, 437)
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    eng.set_text_features(T.numpy(), seg)
+    out = eng.classify(px.to(gpu))
+    torch.cuda.synchronize()
+    f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[name], px)
+    fh, lr, pr, ti, tp = clip_ref.head(f_ref, T, seg)
+    cos = torch.nn.functional.cosine_similarity(out.emb.cpu(), fh, dim=-1)
+    assert cos.min() > 0.9995, cos
+    rel = _check_logits(out.logits.cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[dtype])
+    # probabilities within each segment
+    assert np.abs(out.probs.cpu().numpy() - pr.numpy()).max() < 5e-3
+    print(f"{name} {dtype} lora={lora}: max rel logit err {rel:.2e}, min cos {cos.min():.6f}")
+
+
+def test_encode_image_unnormalised(gpu):
+    cfg = C.VIT_B32
+    eng, ref_sd = _engine(cfg, "bf16", 0, max_batch=16)
+    px = _pixels(3, 224, seed=2)
+    f = eng.encode_image(px.to(gpu)).cpu()
+    ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES["ViT-B/32"], px)
+    assert (f.norm(dim=-1) / ref.norm(dim=-1) - 1).abs().max() < 5e-3
+    assert torch.nn.functional.cosine_similarity(f, ref).min() > 0.9995
+
+
+def test_full_batch_256_properties(gpu):
+    """bs=256 (the metric's batch): every image equals its own bs=1 result bit-for-bit
+    (per-image independence; rows never mix), and a sample of rows matches the oracle."""
+    cfg = C.VIT_B32
+    eng, ref_sd = _engine(cfg, "bf16", 8, max_batch=256)
+    px = _pixels(256, 224, seed=3).to(gpu)
+    T = _text(cfg.embed_dim, 437)
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    eng.set_text_features(T.numpy(), seg)
+    full = eng.classify(px).logits.clone()
+    for i in (0, 1, 77, 255):
+        one = eng.classify(px[i:i + 1]).logits
+        assert torch.equal(one[0], full[i]), i
+    idx = [0, 100, 255]
+    f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES["ViT-B/32"], px[idx].cpu())
+    _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
+    _check_logits(full[idx].cpu().numpy(), lr.numpy(), seg, 1e-3)
