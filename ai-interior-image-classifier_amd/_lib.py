@@ -21,7 +21,7 @@ EXPORTS = (
     "clipvit_create", "clipvit_load_weights", "clipvit_load_lora", "clipvit_set_text_features",
     "clipvit_encode_image", "clipvit_classify", "clipvit_text_shape", "clipvit_destroy",
     "clipvit_last_error", "clipvit_abi_version", "clipvit_gemm_test", "clipvit_attention_test",
-    "clipvit_profile_forward",
+    "clipvit_profile_forward", "clipvit_gemm_bench",
 )
 
 
@@ -78,6 +78,7 @@ def lib() -> ctypes.CDLL:
             "clipvit_gemm_test": (i, [vp, i, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_attention_test": (i, [vp, i, vp, vp, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),
+            "clipvit_gemm_bench": (i, [i, i, i, i, i, i, i, p_f]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -61,14 +61,27 @@ struct LayerW {
     const float *bqkv, *bout, *bfc, *bproj, *ln1g, *ln1b, *ln2g, *ln2b;
 };
 
-struct Workspace {
+// One lane = the activation buffers for `cap` images + the HIP stream that runs them.
+struct Lane {
     int cap = 0;
     float* x = nullptr;  // [cap*N, D] fp32 residual stream
     void* h = nullptr;   // [cap*N, D] 16-bit LN output; also the attention output
     void* qkv = nullptr; // [cap*N, 3D]
     void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the im2col buffer
     float* f = nullptr;  // [cap, E] projected features
-    hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
+};
+
+// A workspace slot serves one call at a time. A batch of B >= SPLIT_MIN images runs as two
+// independent halves on the two lane streams (forked from / joined into the caller's stream
+// by events), so one half's memory-bound kernels and GEMM tails overlap the other half's
+// GEMMs. Smaller batches run on the caller's stream with lane 0.
+constexpr int kLanes = 2;
+constexpr int SPLIT_MIN = 64;
+struct Workspace {
+    Lane lane[kLanes];
+    hipEvent_t fork = nullptr;
     bool used = false;
 };
 
@@ -110,7 +123,9 @@ struct clipvit_handle {
     std::vector<int> seg_host;
     std::mutex mu;
     std::vector<Workspace*> pool;
-    int var[5] = {0, 0, 0, 0, 0};  // GEMM tile variants: qkv, out, fc, proj, patch
+    // GEMM tile variants per role (qkv, out, fc, proj, patch), from tools/gemm_tune.py sweeps
+    // on MI355X (profiles/); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
+    int var[5] = {8, 14, 13, 14, 14};
 };
 
 static std::string L(int i, const char* leaf) {
@@ -146,28 +161,40 @@ static void expected_tensors(const clipvit_handle* h,
 
 static int free_ws(Workspace* w) {
     if (!w) return 0;
-    hipFree(w->x);
-    hipFree(w->h);
-    hipFree(w->qkv);
-    hipFree(w->u);
-    hipFree(w->f);
-    if (w->done) hipEventDestroy(w->done);
+    for (auto& l : w->lane) {
+        hipFree(l.x);
+        hipFree(l.h);
+        hipFree(l.qkv);
+        hipFree(l.u);
+        hipFree(l.f);
+        if (l.done) hipEventDestroy(l.done);
+        if (l.stream) hipStreamDestroy(l.stream);
+    }
+    if (w->fork) hipEventDestroy(w->fork);
     delete w;
     return 0;
 }
 
+static int lane_cap(const clipvit_handle* h) {
+    const int half = (h->cfg.max_batch + 1) / 2;
+    return std::max(half, std::min(h->cfg.max_batch, SPLIT_MIN - 1));
+}
+
 static int alloc_ws(clipvit_handle* h, Workspace** out) {
     Workspace* w = new Workspace();
-    w->cap = h->cfg.max_batch;
-    const size_t rows = (size_t)w->cap * h->N;
-    const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)w->cap * h->G2 * h->Kp * 2);
-    hipError_t e = hipSuccess;
-    if (e == hipSuccess) e = hipMalloc(&w->x, rows * h->D * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(&w->h, rows * h->D * 2);
-    if (e == hipSuccess) e = hipMalloc(&w->qkv, rows * 3 * h->D * 2);
-    if (e == hipSuccess) e = hipMalloc(&w->u, ubytes);
-    if (e == hipSuccess) e = hipMalloc((void**)&w->f, (size_t)w->cap * h->E * sizeof(float));
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&w->done, hipEventDisableTiming);
+    hipError_t e = hipEventCreateWithFlags(&w->fork, hipEventDisableTiming);
+    for (auto& l : w->lane) {
+        l.cap = lane_cap(h);
+        const size_t rows = (size_t)l.cap * h->N;
+        const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)l.cap * h->G2 * h->Kp * 2);
+        if (e == hipSuccess) e = hipMalloc(&l.x, rows * h->D * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&l.h, rows * h->D * 2);
+        if (e == hipSuccess) e = hipMalloc(&l.qkv, rows * 3 * h->D * 2);
+        if (e == hipSuccess) e = hipMalloc(&l.u, ubytes);
+        if (e == hipSuccess) e = hipMalloc((void**)&l.f, (size_t)l.cap * h->E * sizeof(float));
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
+    }
     if (e != hipSuccess) {
         free_ws(w);
         g_err = std::string("workspace allocation failed: ") + hipGetErrorString(e);
@@ -177,8 +204,8 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
     return 0;
 }
 
-// Take a free workspace (allocating one if every pooled workspace is busy) and order the
-// caller's stream after that workspace's previous user.
+// Take a free workspace (allocating one if every pooled workspace is busy). Every use of a
+// lane's buffers is ordered after the previous one through the lane's `done` event.
 static int acquire_ws(clipvit_handle* h, hipStream_t s, Workspace** out) {
     Workspace* w = nullptr;
     {
@@ -197,13 +224,12 @@ static int acquire_ws(clipvit_handle* h, hipStream_t s, Workspace** out) {
         std::lock_guard<std::mutex> lk(h->mu);
         h->pool.push_back(w);
     }
-    HIPCHK(hipStreamWaitEvent(s, w->done, 0));
+    (void)s;
     *out = w;
     return 0;
 }
 
-static void release_ws(clipvit_handle* h, hipStream_t s, Workspace* w) {
-    hipEventRecord(w->done, s);
+static void release_ws(clipvit_handle* h, Workspace* w) {
     std::lock_guard<std::mutex> lk(h->mu);
     w->used = false;
 }
@@ -214,7 +240,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
-    if (launch_gemm(s, h->dt, epi, a, variant) != 0) {
+    // a tuned variant that does not tile this shape falls back to the shape-based choice
+    if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
                 " K=" + std::to_string(K);
         return CLIPVIT_E_INVALID;
@@ -222,9 +249,10 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     return 0;
 }
 
-// Encoder forward for B images; writes the projected (un-normalised) features to f_out.
+// Encoder forward for B images on stream s with lane buffers w; writes the projected
+// (un-normalised) features to f_out.
 static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
-                   Workspace* w, float* f_out, Prof* prof) {
+                   Lane* w, float* f_out, Prof* prof) {
     const int D = h->D, N = h->N, M = B * N;
     int rc;
     if (prof) prof->mark(s, F_EMBED);
@@ -262,6 +290,41 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     if (prof) prof->mark(s, F_HEAD);
     HIPCHK(hipGetLastError());
     return 0;
+}
+
+static size_t pixel_bytes(const clipvit_handle* h, int dtype) {
+    const size_t R = h->cfg.image_size;
+    return 3 * R * R * (dtype == CLIPVIT_F32 ? 4 : 2);
+}
+
+static int lane_batch(int B) { return B >= SPLIT_MIN ? (B + 1) / 2 : B; }
+
+// Run body(stream, lane, first_image, count) for the whole batch: split over the two lane
+// streams (fork/join with the caller's stream s by events) when B >= SPLIT_MIN, otherwise on
+// s itself with lane 0. Lane buffers are always ordered after their previous user.
+template <typename F>
+static int run_lanes(clipvit_handle* h, hipStream_t s, int B, Workspace* w, F&& body) {
+    if (B < SPLIT_MIN) {
+        Lane& l = w->lane[0];
+        HIPCHK(hipStreamWaitEvent(s, l.done, 0));
+        const int rc = body(s, &l, 0, B);
+        HIPCHK(hipEventRecord(l.done, s));
+        return rc;
+    }
+    HIPCHK(hipEventRecord(w->fork, s));
+    const int b0 = (B + 1) / 2;
+    int rc = 0;
+    for (int i = 0; i < kLanes; ++i) {
+        Lane& l = w->lane[i];
+        const int off = i == 0 ? 0 : b0, cnt = i == 0 ? b0 : B - b0;
+        HIPCHK(hipStreamWaitEvent(l.stream, w->fork, 0));
+        HIPCHK(hipStreamWaitEvent(l.stream, l.done, 0));
+        if (!rc) rc = body(l.stream, &l, off, cnt);
+        HIPCHK(hipEventRecord(l.done, l.stream));
+        HIPCHK(hipStreamWaitEvent(s, l.done, 0));
+    }
+    (void)h;
+    return rc;
 }
 
 static int check_call(clipvit_handle* h, const void* pix, int dtype, int B) {
@@ -515,8 +578,12 @@ int clipvit_encode_image(clipvit_handle* h, void* stream, const void* pixels_dev
     hipStream_t s = (hipStream_t)stream;
     Workspace* w = nullptr;
     if ((rc = acquire_ws(h, s, &w))) return rc;
-    rc = forward(h, s, pixels_dev, dtype, B, w, emb_dev, nullptr);
-    release_ws(h, s, w);
+    const size_t pxb = pixel_bytes(h, dtype);
+    rc = run_lanes(h, s, B, w, [&](hipStream_t st, Lane* l, int off, int cnt) {
+        return forward(h, st, (const char*)pixels_dev + off * pxb, dtype, cnt, l, emb_dev + (size_t)off * h->E,
+                       nullptr);
+    });
+    release_ws(h, w);
     return rc;
 }
 
@@ -532,19 +599,26 @@ int clipvit_classify(clipvit_handle* h, void* stream, const void* pixels_dev, in
     hipStream_t s = (hipStream_t)stream;
     Workspace* w = nullptr;
     if ((rc = acquire_ws(h, s, &w))) return rc;
-    rc = forward(h, s, pixels_dev, dtype, B, w, w->f, nullptr);
-    if (!rc) {
-        launch_logits(s, w->f, h->Tt, emb_dev, logits_dev, B, h->E, h->C, h->Cpad);
+    const size_t pxb = pixel_bytes(h, dtype);
+    const size_t C = h->C, E = h->E, T5 = (size_t)h->nseg * 5;
+    rc = run_lanes(h, s, B, w, [&](hipStream_t st, Lane* l, int off, int cnt) {
+        int r = forward(h, st, (const char*)pixels_dev + off * pxb, dtype, cnt, l, l->f, nullptr);
+        if (r) return r;
+        launch_logits(st, l->f, h->Tt, emb_dev ? emb_dev + off * E : nullptr, logits_dev + off * C, cnt, h->E,
+                      h->C, h->Cpad);
         if (probs_dev || top_idx || top_prob)
-            launch_seg_softmax_topk(s, logits_dev, probs_dev, top_idx, top_prob, h->seg_dev, h->nseg, B,
+            launch_seg_softmax_topk(st, logits_dev + off * C, probs_dev ? probs_dev + off * C : nullptr,
+                                    top_idx ? top_idx + off * T5 : nullptr,
+                                    top_prob ? top_prob + off * T5 : nullptr, h->seg_dev, h->nseg, cnt,
                                     h->C);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
             g_err = std::string("head launch failed: ") + hipGetErrorString(e);
-            rc = CLIPVIT_E_HIP;
+            return CLIPVIT_E_HIP;
         }
-    }
-    release_ws(h, s, w);
+        return 0;
+    });
+    release_ws(h, w);
     return rc;
 }
 
@@ -558,6 +632,11 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
     hipStream_t s = (hipStream_t)stream;
     Workspace* w = nullptr;
     if ((rc = acquire_ws(h, s, &w))) return rc;
+    // One lane's forward, serialised on the caller's stream, at the per-lane batch the split
+    // path launches (ceil(B/2) for B >= SPLIT_MIN): per-launch kernel times, no overlap.
+    const int Bl = std::min(lane_batch(B), w->lane[0].cap);
+    Lane* l = &w->lane[0];
+    HIPCHK(hipStreamWaitEvent(s, l->done, 0));
     Prof p;
     const size_t nmarks = 8 + 8 * (size_t)h->cfg.layers;
     p.ev.resize(nmarks);
@@ -566,7 +645,7 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
     double acc[F_COUNT] = {0};
     for (int it = 0; it < iters && !rc; ++it) {
         p.k = 0;
-        rc = forward(h, s, pixels_dev, dtype, B, w, w->f, &p);
+        rc = forward(h, s, pixels_dev, dtype, Bl, l, l->f, &p);
         if (rc) break;
         hipEventSynchronize(p.ev[p.k - 1]);
         for (size_t k = 1; k < p.k; ++k) {
@@ -575,9 +654,11 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
             acc[p.fam[k]] += ms;
         }
     }
+    hipEventRecord(l->done, s);
     for (auto& e : p.ev) hipEventDestroy(e);
-    release_ws(h, s, w);
+    release_ws(h, w);
     for (int f = 0; f < F_COUNT; ++f) out_ms[f] = (float)(acc[f] / iters);
+    out_ms[F_COUNT] = (float)Bl;
     return rc;
 }
 
@@ -619,6 +700,47 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     const int rc = launch_gemm(s, dtype, e, a, variant);
     HIPCHK(hipFreeAsync(Wp, s));
     if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int iters,
+                       float* avg_ms) {
+    g_err.clear();
+    if (!avg_ms || iters <= 0 || K % 64 || N % 64 || M <= 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
+    void *A = nullptr, *W = nullptr, *Cb = nullptr;
+    float* bias = nullptr;
+    HIPCHK(hipMalloc(&A, (size_t)M * K * 2));
+    HIPCHK(hipMalloc(&W, (size_t)N * K * 2));
+    HIPCHK(hipMalloc(&Cb, (size_t)M * N * 4));
+    HIPCHK(hipMalloc(&bias, (size_t)N * 4));
+    launch_fill_random16(nullptr, dtype, A, (size_t)M * K, 1u);
+    launch_fill_random16(nullptr, dtype, W, (size_t)N * K, 2u);
+    HIPCHK(hipMemset(bias, 0, (size_t)N * 4));
+    HIPCHK(hipMemset(Cb, 0, (size_t)M * N * 4));
+    GemmArgs a{};
+    a.A = A; a.W = W; a.bias = bias; a.C = Cb;
+    a.M = M; a.N = N; a.K = K; a.ldc = N;
+    a.patch_g2 = 49; a.patch_ntok = 50;
+    const int e = epi;  // raw Epi enum
+    int rc = launch_gemm(nullptr, dtype, e, a, variant);
+    hipEvent_t t0, t1;
+    hipEventCreate(&t0);
+    hipEventCreate(&t1);
+    hipEventRecord(t0, nullptr);
+    for (int i = 0; i < iters && !rc; ++i) rc = launch_gemm(nullptr, dtype, e, a, variant);
+    hipEventRecord(t1, nullptr);
+    hipEventSynchronize(t1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, t0, t1);
+    hipEventDestroy(t0);
+    hipEventDestroy(t1);
+    *avg_ms = ms / iters;
+    hipFree(A);
+    hipFree(W);
+    hipFree(Cb);
+    hipFree(bias);
+    if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported variant/shape");
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -97,6 +97,7 @@ void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const f
                       const float* b, int rows, int D);
 void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,
                         int Kp);
+void launch_fill_random16(hipStream_t s, int dtype, void* p, size_t n, unsigned seed);
 void launch_lora_merge(hipStream_t s, float* W, const float* A, const float* Bm, int in_f,
                        int out_f, int rank, float scaling);
 void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,

@@ -167,6 +167,226 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_nt_kernel(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Pipelined variant: an NS-stage LDS ring (BK = 64) filled by global_load_lds; loads of up to
+// NS-1 tiles stay in flight ACROSS barriers (raw s_barrier + hand-counted vmcnt, never
+// __syncthreads(), which would drain vmcnt to 0); fragments for the next 32-deep k-substep
+// are read from LDS while the current substep's MFMAs run, and the barrier that hands over
+// tile kt+1 sits between the last ds_read of tile kt and its last MFMAs.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until the awaited tile's loads have landed, given r = number of tiles (LPT loads each)
+// issued after it that may stay in flight (0 <= r <= NS - 2).
+template <int LPT, int NS>
+__device__ __forceinline__ void wait_tile(int r) {
+    if constexpr (NS - 2 >= 2) {
+        if (r >= 2) { vm_wait<2 * LPT>(); return; }
+    }
+    if constexpr (NS - 2 >= 1) {
+        if (r >= 1) { vm_wait<LPT>(); return; }
+    }
+    vm_wait<0>();
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+__global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(TN % 64 == 0 && TM % 16 == 0, "wave tile");
+    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
+    constexpr int LA = A_BYTES / (NT * 16), LW = W_BYTES / (NT * 16);
+    static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "staging rounds");
+    constexpr int LPT = LA + LW;  // glds per thread per tile
+    constexpr int STAGE = A_BYTES + W_BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int nN = a.N / BN;
+    const int nwg = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
+
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K * 2;
+    const int mlast = a.M - 1;
+    // per-thread source row offsets (constant over k)
+    size_t asrc[LA], wsrc[LW];
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
+        asrc[r] = (size_t)min(m0 + row, mlast) * ldb + c * 16;
+    }
+#pragma unroll
+    for (int r = 0; r < LW; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
+        wsrc[r] = (size_t)(n0 + row) * ldb + c * 16;
+    }
+    auto stage = [&](int buf, int kt) {
+        unsigned char* sA = smem + buf * STAGE;
+        unsigned char* sW = sA + A_BYTES;
+        const size_t kofs = (size_t)kt * 128;
+#pragma unroll
+        for (int r = 0; r < LA; ++r) glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
+#pragma unroll
+        for (int r = 0; r < LW; ++r) glds16(Wb + wsrc[r] + kofs, sW + r * NT * 16 + wave * 1024);
+    };
+
+    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
+    const int aoff = (wm * TM + lrow) * 128, woff = A_BYTES + (wn * TN + lrow) * 128;
+    auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
+        const unsigned char* base = smem + buf * STAGE;
+        const int c = (((s << 2) | lg) ^ lsw) << 4;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + c);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + c);
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // Ring protocol: tile t lives in stage t % NS. Prologue issues tiles 0..NS-2; the stage of
+    // tile t-1 is refilled with tile t-1+NS right after the barrier that follows every wave's
+    // last ds_read of tile t-1 (lgkmcnt(0) before that barrier).
+    const int nk = a.K >> 6;
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) stage(s, s);
+    wait_tile<LPT, NS>(min(NS - 2, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    if (NS - 1 < nk) stage(NS - 1, NS - 1);
+
+    constexpr int NFR = FM + FN;        // ds_read_b128 per substep
+    constexpr int NMF = FM * FN;        // MFMAs per substep
+    // interleave the NFR reads of the next substep one-per-MFMA among this substep's MFMAs
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF - NFR, 0);
+    };
+    static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
+
+    auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+    };
+
+    vec8 a0[FM], w0[FN], a1[FM], w1[FN];
+    load_frags(0, 0, a0, w0);
+    for (int kt = 0; kt < nk - 1; ++kt) {   // steady state: branch-free around the LDS reads
+        const int cur = kt % NS;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): a0/w0 (read one MFMA block ago) landed
+        load_frags(cur, 1, a1, w1);
+        mfmas(a0, w0);
+        interleave();
+        __builtin_amdgcn_s_waitcnt(0xC07F);                  // a1/w1 landed: stage kt fully read
+        wait_tile<LPT, NS>(min(NS - 2, nk - 2 - kt));       // tile kt+1 landed (own loads)
+        __builtin_amdgcn_s_barrier();                        // ... and everyone else's
+        if (kt + NS < nk) stage(cur, kt + NS);               // refill the stage just freed
+        load_frags((kt + 1) % NS, 0, a0, w0);
+        mfmas(a1, w1);
+        interleave();
+    }
+    {   // last tile
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        load_frags((nk - 1) % NS, 1, a1, w1);
+        mfmas(a0, w0);
+        interleave();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        mfmas(a1, w1);
+    }
+
+    // ---- epilogue (same contract as gemm_nt_kernel) ----
+    const int g = lg;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = m0 + wm * TM + fm * 16 + lrow;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int q = 0; q < FN / 4; ++q) {
+            const int n = n0 + wn * TN + q * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
+            if constexpr (EPI != EPI_PATCH) {
+                if (a.bias) {
+                    const float4* b4 = (const float4*)(a.bias + n);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 bb = b4[i];
+                        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                    }
+                }
+            }
+            if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+            }
+            if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+                dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                    pack2<T>(v[6], v[7]));
+                dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                    pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+            } else if constexpr (EPI == EPI_RESID) {
+                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float4 o = dst[i];
+                    o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                    dst[i] = o;
+                }
+            } else {
+                size_t row = (size_t)m;
+                if constexpr (EPI == EPI_PATCH)
+                    row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
+                float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        }
+    }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS>
+static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
+    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+    dim3 grid(nwg), block(64 * WM * WN);
+    switch (epi) {
+        case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+        case EPI_PATCH: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+    }
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 static void launch_tile(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
@@ -209,6 +429,47 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         case 4:
             if (a.N % 64) return -1;
             launch_tile<T, 64, 64, 4, 1>(s, epi, a);
+            return 0;
+        case 5:
+            if (a.N % 256) return -1;
+            launch_tile<T, 128, 256, 2, 4>(s, epi, a);
+            return 0;
+        case 6:
+            if (a.N % 128) return -1;
+            launch_tile<T, 256, 128, 2, 2>(s, epi, a);
+            return 0;
+        case 7:
+            if (a.N % 128) return -1;
+            launch_tile<T, 128, 128, 4, 2>(s, epi, a);
+            return 0;
+        // ---- pipelined ring variants ----
+        case 8:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 256, 256, 2, 4, 2>(s, epi, a);
+            return 0;
+        case 9:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 128, 256, 2, 4, 3>(s, epi, a);
+            return 0;
+        case 10:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 256, 128, 4, 2, 3>(s, epi, a);
+            return 0;
+        case 11:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 128, 128, 2, 2, 2>(s, epi, a);
+            return 0;
+        case 12:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 128, 128, 2, 2, 4>(s, epi, a);
+            return 0;
+        case 13:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 128, 128, 4, 2, 2>(s, epi, a);
+            return 0;
+        case 14:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 192, 256, 2, 4, 2>(s, epi, a);
             return 0;
     }
     return -1;

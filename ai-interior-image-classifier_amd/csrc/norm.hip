@@ -229,6 +229,24 @@ void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, i
     else pack_weight_kernel<BF16><<<blocks, threads, 0, s>>>(src, (u16*)dst, N, K, Kp);
 }
 
+// Uniform [-1, 1) 16-bit fill (benchmark operands: random data, not zeros, so the measured
+// clock is the one real inputs get — cdna_hip_programming.md §5.4 rule 25).
+template <typename T>
+__global__ void fill_random16_kernel(u16* p, size_t n, unsigned seed) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned x = (unsigned)i * 2654435761u ^ (seed * 0x9E3779B9u);
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    p[i] = T::from_f32((float)(x >> 8) * (2.0f / 16777216.0f) - 1.0f);
+}
+
+void launch_fill_random16(hipStream_t s, int dtype, void* p, size_t n, unsigned seed) {
+    const int threads = 256;
+    const size_t blocks = (n + threads - 1) / threads;
+    if (dtype == 2) fill_random16_kernel<F16><<<blocks, threads, 0, s>>>((u16*)p, n, seed);
+    else fill_random16_kernel<BF16><<<blocks, threads, 0, s>>>((u16*)p, n, seed);
+}
+
 // W[o][i] += scaling * sum_r A[i][r] * B[r][o]   (fp32, once at load time)
 __global__ void lora_merge_kernel(float* __restrict__ W, const float* __restrict__ A,
                                   const float* __restrict__ Bm, int in_f, int out_f, int rank,

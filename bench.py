@@ -146,7 +146,8 @@ def main():
 
     # live per-kernel-family device times (HIP events on the launch stream)
     fam = eng.profile_forward(px, iters=a.profile_iters)
-    D, N, M = cfg.width, cfg.tokens, a.batch * cfg.tokens
+    lane_b = int(fam.pop("lane_batch"))  # images per launch (per stream lane)
+    D, N, M = cfg.width, cfg.tokens, lane_b * cfg.tokens
     mlp_flop = 2.0 * M * D * 4 * D  # c_fc and c_proj each
     mlp_ms = (fam["fc_gemm"] + fam["proj_gemm"]) / (2 * cfg.layers)  # per launch
     achieved = mlp_flop / (mlp_ms * 1e-3) / 1e12
@@ -172,7 +173,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj+residual)",
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),
-                     "flop_per_launch": mlp_flop, "avg_launch_ms": round(mlp_ms, 5),
+                     "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(mlp_ms, 5),
                      "model_mfma_frac": round(model_tflops / peak, 4),
                      "family_ms_per_forward": {k: round(v, 4) for k, v in fam.items()}},
         "cpu_baseline": None,

@@ -148,15 +148,23 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi,
                       int variant);
 
+/* Average device time (ms) of `iters` back-to-back launches of one GEMM on random uniform
+ * [-1,1) operands allocated inside (tile-variant tuning; epi = internal epilogue enum:
+ * 0 store16, 1 gelu16, 2 resid32, 3 patch32, 4 f32, 5 f32gelu). Default stream. */
+int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int iters,
+                       float* avg_ms);
+
 /* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
  * out [B*N, H*64] of `dtype`. */
 int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B,
                            int N, int H);
 
-/* Time `iters` launches of the encoder forward at batch B on `stream`; returns the
- * average per-kernel-family device time (ms) into out_ms[0..7]:
- * 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm, 5 fc gemm,
- * 6 proj gemm, 7 head. Requires weights loaded. Used by bench.py's roofline probe. */
+/* Time `iters` launches of ONE lane's encoder forward (the per-stream batch the call path
+ * launches for B images: ceil(B/2) when the batch is split over the two lane streams, else B)
+ * serialised on `stream`; returns the average per-kernel-family device time (ms) into
+ * out_ms[0..7]: 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm,
+ * 5 fc gemm, 6 proj gemm, 7 head (ln_post+proj); out_ms[8] = the lane batch profiled.
+ * Requires weights loaded. Used by bench.py's roofline probe. */
 int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype,
                             int B, int iters, float* out_ms);
 
