@@ -78,7 +78,9 @@ struct Lane {
 // by events), so one half's memory-bound kernels and GEMM tails overlap the other half's
 // GEMMs. Smaller batches run on the caller's stream with lane 0.
 constexpr int kLanes = 2;
-constexpr int SPLIT_MIN = 64;
+// Off by default: measured on MI355X, the half-batch GEMMs lose more to tile quantization
+// than the two lanes gain from overlapping (profiles/r01_*). CLIPVIT_SPLIT_MIN=n enables it.
+constexpr int SPLIT_NEVER = 1 << 30;
 struct Workspace {
     Lane lane[kLanes];
     hipEvent_t fork = nullptr;
@@ -126,6 +128,7 @@ struct clipvit_handle {
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from tools/gemm_tune.py sweeps
     // on MI355X (profiles/); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
     int var[5] = {8, 14, 13, 14, 14};
+    int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
 };
 
 static std::string L(int i, const char* leaf) {
@@ -177,7 +180,7 @@ static int free_ws(Workspace* w) {
 
 static int lane_cap(const clipvit_handle* h) {
     const int half = (h->cfg.max_batch + 1) / 2;
-    return std::max(half, std::min(h->cfg.max_batch, SPLIT_MIN - 1));
+    return std::max(half, std::min(h->cfg.max_batch, h->split_min - 1));
 }
 
 static int alloc_ws(clipvit_handle* h, Workspace** out) {
@@ -297,14 +300,16 @@ static size_t pixel_bytes(const clipvit_handle* h, int dtype) {
     return 3 * R * R * (dtype == CLIPVIT_F32 ? 4 : 2);
 }
 
-static int lane_batch(int B) { return B >= SPLIT_MIN ? (B + 1) / 2 : B; }
+static int lane_batch(const clipvit_handle* h, int B) {
+    return B >= h->split_min ? (B + 1) / 2 : B;
+}
 
 // Run body(stream, lane, first_image, count) for the whole batch: split over the two lane
 // streams (fork/join with the caller's stream s by events) when B >= SPLIT_MIN, otherwise on
 // s itself with lane 0. Lane buffers are always ordered after their previous user.
 template <typename F>
 static int run_lanes(clipvit_handle* h, hipStream_t s, int B, Workspace* w, F&& body) {
-    if (B < SPLIT_MIN) {
+    if (B < h->split_min) {
         Lane& l = w->lane[0];
         HIPCHK(hipStreamWaitEvent(s, l.done, 0));
         const int rc = body(s, &l, 0, B);
@@ -383,6 +388,10 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->K3 = 3 * c.patch_size * c.patch_size;
     h->Kp = (h->K3 + 63) / 64 * 64;
     h->dt = c.compute_dtype;
+    if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
+        h->split_min = atoi(v);
+        if (h->split_min <= 0) h->split_min = SPLIT_NEVER;
+    }
     if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
         int k = 0;
         for (const char* p = v; *p && k < 5; ++k) {
@@ -634,7 +643,7 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
     if ((rc = acquire_ws(h, s, &w))) return rc;
     // One lane's forward, serialised on the caller's stream, at the per-lane batch the split
     // path launches (ceil(B/2) for B >= SPLIT_MIN): per-launch kernel times, no overlap.
-    const int Bl = std::min(lane_batch(B), w->lane[0].cap);
+    const int Bl = std::min(lane_batch(h, B), w->lane[0].cap);
     Lane* l = &w->lane[0];
     HIPCHK(hipStreamWaitEvent(s, l->done, 0));
     Prof p;

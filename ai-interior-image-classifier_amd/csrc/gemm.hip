@@ -373,6 +373,206 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Ping-pong GEMM (the production kernel): 256x256 block tile, BK = 32, 8 waves in two groups
+// of 4 that run one barrier apart. Group g owns token rows [128 g, 128 g + 128); wave p of a
+// group owns features [64 p, 64 p + 64) -> 8 x 4 accumulator tiles of 16x16 per wave.
+// Every barrier interval, on every SIMD, one wave issues a 16-MFMA cluster while its partner
+// (the other group) reads its next fragments from LDS and issues its share of the
+// global->LDS loads, so the matrix pipe never waits on LDS or on a barrier of its own group.
+//   per tile, group g:  R0 | M0 | R1 | M1      (R = read phase, M = 16-MFMA cluster)
+//   group 1 starts one interval late (one extra s_barrier first; group 0 one extra last).
+// LDS: 4-stage ring of 32 KB (A 256 x 32 + W 256 x 32, 16-bit); tile t+3 is loaded while tile t
+// is consumed (group 0 loads A rows, group 1 loads W rows, half a tile per read phase), so
+// every global load has ~9 intervals to land. Rows are 64 B: 16-B chunk c of row r is stored at
+// c ^ ((r >> 2) & 2), which makes each ds_read_b128 fragment read conflict-free; glds writes
+// lane-linearly, so the same permutation is applied to the per-lane SOURCE address.
+constexpr int PP_BM = 256, PP_BN = 256, PP_NS = 4, PP_STAGE = 32768;
+
+__device__ __forceinline__ void sbar() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// ABL (timing-only ablation builds, results wrong): bit0 no global->LDS loads in the loop,
+// bit1 no LDS fragment reads in the loop, bit2 no barriers in the loop.
+template <typename T, int EPI, int ABL = 0>
+__global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[PP_NS * PP_STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = wave >> 2, p = wave & 3;
+    const int nN = a.N / PP_BN;
+    const int nwg = gridDim.x;
+    int bid = blockIdx.x;
+    {
+        const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    }
+    const int m0 = (bid / nN) * PP_BM, n0 = (bid % nN) * PP_BN;
+    const size_t ldb = (size_t)a.K * 2;
+    const int nk = a.K >> 5;
+
+    // ---- global->LDS assignment: group 0 loads A (rows m0..), group 1 loads W (rows n0..);
+    // read phase r loads rows [128 r, 128 r + 128) of that operand, 2 x 16 B per thread.
+    const unsigned char* src_base = (const unsigned char*)(g == 0 ? a.A : a.W);
+    const int tg = tid & 255;
+    size_t srcoff[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int row = r * 128 + j * 64 + (tg >> 2);
+            const int c = (tg & 3) ^ ((row >> 2) & 2);
+            const int grow = g == 0 ? min(m0 + row, a.M - 1) : n0 + row;
+            srcoff[r][j] = (size_t)grow * ldb + c * 16;
+        }
+    const int ldsw = g * 16384 + (wave & 3) * 1024;  // wave-uniform part of the glds target
+    auto issue = [&](int r, int t) {  // half-tile r of K-tile t into its ring stage
+        unsigned char* dst = smem + (t % PP_NS) * PP_STAGE + ldsw + r * 8192;
+        const size_t kofs = (size_t)t * 64;
+        glds16(src_base + srcoff[r][0] + kofs, dst);
+        glds16(src_base + srcoff[r][1] + kofs, dst + 4096);
+    };
+
+    // ---- fragment addressing (see swizzle note above)
+    const int cs = (((lane >> 4) ^ ((lane >> 2) & 2)) << 4);
+    const int arow = (g * 128 + (lane & 15)) * 64 + cs;
+    const int wrow = 16384 + (p * 64 + (lane & 15)) * 64 + cs;
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    vec8 af[4], wf[4];
+
+    // ---- prologue: tiles 0..2 in flight, wait for tile 0 (own loads), publish
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+        if (t < nk) { issue(0, t); issue(1, t); }
+    if (nk >= 3) vm_wait<8>();
+    else if (nk == 2) vm_wait<4>();
+    else vm_wait<0>();
+    sbar();
+    if (g == 1 && !(ABL & 4)) sbar();  // stagger: group 1 runs one interval behind
+
+    for (int t = 0; t < nk; ++t) {
+        const unsigned char* st = smem + (t % PP_NS) * PP_STAGE;
+        const bool more = (ABL & 1) ? false : t + 3 < nk;
+        // R0: fragments for cluster 0 (A rows 0-63 of the group, all W), first half-load of t+3
+        if (!(ABL & 2) || t == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = *(const vec8*)(st + arow + i * 1024);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) wf[i] = *(const vec8*)(st + wrow + i * 1024);
+        }
+        if (more) issue(0, t + 3);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (!(ABL & 4)) sbar();
+        // M0
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < 4; ++fn) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+        if (!(ABL & 4)) sbar();
+        // R1: fragments for cluster 1 (A rows 64-127), second half-load of t+3, tile t+1 landed
+        if (!(ABL & 2)) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) af[i] = *(const vec8*)(st + arow + (4 + i) * 1024);
+        }
+        if (more) issue(1, t + 3);
+        {
+            const int after = min(2, nk - 2 - t);  // tiles issued after t+1 (4 loads each)
+            if (after >= 2) vm_wait<8>();
+            else if (after == 1) vm_wait<4>();
+            else vm_wait<0>();
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        if (!(ABL & 4)) sbar();
+        // M1
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < 4; ++fn)
+                acc[fn][4 + fm] = T::mfma16(wf[fn], af[fm], acc[fn][4 + fm]);
+        __builtin_amdgcn_s_setprio(0);
+        if (!(ABL & 4)) sbar();
+    }
+    if (g == 0 && !(ABL & 4)) sbar();  // balance the stagger barrier
+
+    // ---- epilogue: lane owns token m and features n .. n+15 of each 64-feature group
+    const int lg = lane >> 4, lrow = lane & 15;
+#pragma unroll
+    for (int fm = 0; fm < 8; ++fm) {
+        const int m = m0 + g * 128 + fm * 16 + lrow;
+        if (m >= a.M) continue;
+        const int n = n0 + p * 64 + 16 * lg;
+        float v[16];
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[f][fm][r];
+        if constexpr (EPI != EPI_PATCH) {
+            if (a.bias) {
+                const float4* b4 = (const float4*)(a.bias + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 bb = b4[i];
+                    v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                }
+            }
+        }
+        if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+        }
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+            uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+            dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                pack2<T>(v[6], v[7]));
+            dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
+                                pack2<T>(v[14], v[15]));
+        } else if constexpr (EPI == EPI_RESID) {
+            float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float4 o = dst[i];
+                o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                dst[i] = o;
+            }
+        } else {
+            size_t row = (size_t)m;
+            if constexpr (EPI == EPI_PATCH)
+                row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
+            float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        }
+    }
+}
+
+template <typename T>
+static void launch_pp(hipStream_t s, int epi, const GemmArgs& a) {
+    const int nwg = (a.N / PP_BN) * ((a.M + PP_BM - 1) / PP_BM);
+    dim3 grid(nwg), block(512);
+    switch (epi) {
+        case EPI_STORE: gemm_pp_kernel<T, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU: gemm_pp_kernel<T, EPI_GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_pp_kernel<T, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+        case EPI_PATCH: gemm_pp_kernel<T, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: gemm_pp_kernel<T, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32GELU: gemm_pp_kernel<T, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+    }
+}
+
 template <typename T, int BM, int BN, int WM, int WN, int NS>
 static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
@@ -471,6 +671,23 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 256) return -1;
             launch_pipe<T, 192, 256, 2, 4, 2>(s, epi, a);
             return 0;
+        case 15:
+            if (a.N % 256 || a.K % 32) return -1;
+            launch_pp<T>(s, epi, a);
+            return 0;
+        case 16: case 17: case 18: case 19: case 20: {  // ablations (timing only)
+            if (a.N % 256 || a.K % 32) return -1;
+            const int nwg = (a.N / PP_BN) * ((a.M + PP_BM - 1) / PP_BM);
+            const int abl[5] = {1, 2, 4, 3, 7};
+            switch (abl[variant - 16]) {
+                case 1: gemm_pp_kernel<T, EPI_F32, 1><<<nwg, 512, 0, s>>>(a); break;
+                case 2: gemm_pp_kernel<T, EPI_F32, 2><<<nwg, 512, 0, s>>>(a); break;
+                case 4: gemm_pp_kernel<T, EPI_F32, 4><<<nwg, 512, 0, s>>>(a); break;
+                case 3: gemm_pp_kernel<T, EPI_F32, 3><<<nwg, 512, 0, s>>>(a); break;
+                case 7: gemm_pp_kernel<T, EPI_F32, 7><<<nwg, 512, 0, s>>>(a); break;
+            }
+            return 0;
+        }
     }
     return -1;
 }

@@ -5,25 +5,54 @@
 //   probs  = softmax(logits) inside each label segment      (detector 40 | styles | ... )
 //   top-k  = topk(min(5, n)) per segment                    main.py:211, main.py:457, main.py:507
 // T rows are the cached, already L2-normalised text features (main.py:179-182, 296-311); the
-// library keeps them transposed (Tt [E][Cpad]) so the logit loop reads them coalesced.
+// library keeps them transposed (Tt [E][Cpad]) so column tiles load coalesced.
+//
+// Both matrix products are small (B x 768 x 512 and B x 512 x 437): each workgroup computes a
+// 16-image x 64-column tile, streaming the weight operand through LDS in 64-deep chunks with
+// float4 loads (no per-iteration global-load latency), 4 images x 1 column per thread.
 #include "common.h"
 
 namespace clipvit {
 
-constexpr int HEAD_ROWS = 16;  // images per workgroup
+constexpr int HR = 16;   // images per workgroup
+constexpr int HK = 64;   // reduction chunk
 
-// grid (ceil(B/16), E/64), 256 threads.  LN of 16 CLS rows into LDS, then each thread
-// accumulates 4 images x 1 output column over D.
+// acc[i] += sum_k X[ib + i][k] * W[k][col]  for k in [0, K), X in LDS [HR][K], W global [K][ldw]
+__device__ __forceinline__ void tile_accumulate(const float* __restrict__ xs, int K,
+                                                const float* __restrict__ W, int ldw, int col0,
+                                                float* ws, float (&acc)[4], int tid) {
+    const int tx = tid & 63, ib = (tid >> 6) * 4;
+    for (int k0 = 0; k0 < K; k0 += HK) {
+        __syncthreads();
+        // 64 x 64 chunk of W: thread loads 4 float4 (rows k0 + (tid >> 4) + 16 j, cols 4 (tid & 15))
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int r = (tid >> 4) + 16 * j, c = (tid & 15) * 4;
+            *(float4*)(ws + r * 68 + c) = *(const float4*)(W + (size_t)(k0 + r) * ldw + col0 + c);
+        }
+        __syncthreads();
+#pragma unroll 16
+        for (int k = 0; k < HK; ++k) {
+            const float w = ws[k * 68 + tx];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[i] += xs[(ib + i) * K + k0 + k] * w;
+        }
+    }
+}
+
+// grid (ceil(B/16), E/64), 256 threads.
 __global__ __launch_bounds__(256) void cls_ln_proj_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ gm,
                                                           const float* __restrict__ bt,
                                                           const float* __restrict__ proj,
                                                           float* __restrict__ f, int B, int N,
                                                           int D, int E) {
-    extern __shared__ __attribute__((aligned(16))) float ys[];  // [16][D]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][D] + [64][68]
+    float* ys = sm;
+    float* ws = sm + HR * D;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * HEAD_ROWS;
-    for (int i = wave; i < HEAD_ROWS; i += 4) {
+    const int b0 = blockIdx.x * HR;
+    for (int i = wave; i < HR; i += 4) {  // LayerNorm of the CLS rows (one wave per row)
         const int b = b0 + i;
         float* yr = ys + i * D;
         if (b >= B) {
@@ -42,19 +71,14 @@ __global__ __launch_bounds__(256) void cls_ln_proj_kernel(const float* __restric
         const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
         for (int c = lane; c < D; c += 64) yr[c] = (xr[c] - mean) * rstd * gm[c] + bt[c];
     }
-    __syncthreads();
-    const int e = blockIdx.y * 64 + lane;
-    const int ib = wave * 4;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int d = 0; d < D; ++d) {
-        const float p = proj[(size_t)d * E + e];
+    const int col0 = blockIdx.y * 64;
+    tile_accumulate(ys, D, proj, E, col0, ws, acc, tid);
+    const int ib = wave * 4;
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) acc[ii] += ys[(ib + ii) * D + d] * p;
-    }
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii) {
-        const int b = b0 + ib + ii;
-        if (b < B) f[(size_t)b * E + e] = acc[ii];
+    for (int i = 0; i < 4; ++i) {
+        const int b = b0 + ib + i;
+        if (b < B) f[(size_t)b * E + col0 + lane] = acc[i];
     }
 }
 
@@ -64,10 +88,12 @@ __global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ f
                                                      float* __restrict__ emb_norm,
                                                      float* __restrict__ logits, int B, int E,
                                                      int C, int Cpad) {
-    extern __shared__ __attribute__((aligned(16))) float fs[];  // [16][E]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][E] + [64][68]
+    float* fs = sm;
+    float* ws = sm + HR * E;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * HEAD_ROWS;
-    for (int i = wave; i < HEAD_ROWS; i += 4) {
+    const int b0 = blockIdx.x * HR;
+    for (int i = wave; i < HR; i += 4) {
         const int b = b0 + i;
         float* fr = fs + i * E;
         if (b >= B) {
@@ -84,33 +110,33 @@ __global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ f
             if (emb_norm && blockIdx.y == 0) emb_norm[(size_t)b * E + c] = v;
         }
     }
-    __syncthreads();
-    const int c = blockIdx.y * 64 + lane;
-    const int ib = wave * 4;
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int e = 0; e < E; ++e) {
-        const float t = Tt[(size_t)e * Cpad + c];
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) acc[ii] += fs[(ib + ii) * E + e] * t;
-    }
+    const int col0 = blockIdx.y * 64;
+    tile_accumulate(fs, E, Tt, Cpad, col0, ws, acc, tid);
+    const int c = col0 + lane, ib = wave * 4;
     if (c < C) {
 #pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-            const int b = b0 + ib + ii;
-            if (b < B) logits[(size_t)b * C + c] = 100.0f * acc[ii];
+        for (int i = 0; i < 4; ++i) {
+            const int b = b0 + ib + i;
+            if (b < B) logits[(size_t)b * C + c] = 100.0f * acc[i];
         }
     }
 }
 
-// grid B, one wave per image: per segment softmax and top-min(5, n) (ties -> lower index).
-__global__ __launch_bounds__(64) void seg_softmax_topk_kernel(const float* __restrict__ logits,
-                                                              float* __restrict__ probs,
-                                                              int* __restrict__ top_idx,
-                                                              float* __restrict__ top_prob,
-                                                              const int* __restrict__ seg_off,
-                                                              int nseg, int C) {
-    const int b = blockIdx.x, lane = threadIdx.x;
-    const float* lr = logits + (size_t)b * C;
+// One wave per image; the image's logits row is staged in LDS once, then every segment's
+// max / sum / top-min(5, n) (ties -> lower index, like a stable sort) runs from LDS.
+constexpr int SM_WAVES = 4;
+__global__ __launch_bounds__(64 * SM_WAVES) void seg_softmax_topk_kernel(
+    const float* __restrict__ logits, float* __restrict__ probs, int* __restrict__ top_idx,
+    float* __restrict__ top_prob, const int* __restrict__ seg_off, int nseg, int B, int C) {
+    extern __shared__ __attribute__((aligned(16))) float rows[];  // [SM_WAVES][C]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x * SM_WAVES + wave;
+    if (b >= B) return;
+    float* lr = rows + wave * C;
+    const float* src = logits + (size_t)b * C;
+    for (int c = lane; c < C; c += 64) lr[c] = src[c];
+    __builtin_amdgcn_s_waitcnt(0);  // own wave's LDS writes visible to its own later reads
     for (int sg = 0; sg < nseg; ++sg) {
         const int s0 = seg_off[sg], s1 = seg_off[sg + 1], n = s1 - s0;
         float m = -INFINITY;
@@ -155,21 +181,31 @@ __global__ __launch_bounds__(64) void seg_softmax_topk_kernel(const float* __res
 
 void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,
                         const float* proj, float* f, int B, int N, int D, int E) {
-    dim3 grid((B + HEAD_ROWS - 1) / HEAD_ROWS, E / 64), block(256);
-    cls_ln_proj_kernel<<<grid, block, HEAD_ROWS * D * sizeof(float), s>>>(x, g, b, proj, f, B, N,
-                                                                          D, E);
+    static const bool attr = hipFuncSetAttribute((const void*)cls_ln_proj_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024) == hipSuccess;
+    (void)attr;
+    dim3 grid((B + HR - 1) / HR, E / 64), block(256);
+    const size_t lds = (HR * D + 64 * 68) * sizeof(float);
+    cls_ln_proj_kernel<<<grid, block, lds, s>>>(x, g, b, proj, f, B, N, D, E);
 }
 
 void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_norm, float* logits,
                    int B, int E, int C, int Cpad) {
-    dim3 grid((B + HEAD_ROWS - 1) / HEAD_ROWS, Cpad / 64), block(256);
-    logits_kernel<<<grid, block, HEAD_ROWS * E * sizeof(float), s>>>(f, Tt, emb_norm, logits, B, E,
-                                                                     C, Cpad);
+    static const bool attr = hipFuncSetAttribute((const void*)logits_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024) == hipSuccess;
+    (void)attr;
+    dim3 grid((B + HR - 1) / HR, Cpad / 64), block(256);
+    const size_t lds = (HR * E + 64 * 68) * sizeof(float);
+    logits_kernel<<<grid, block, lds, s>>>(f, Tt, emb_norm, logits, B, E, C, Cpad);
 }
 
 void launch_seg_softmax_topk(hipStream_t s, const float* logits, float* probs, int* top_idx,
                              float* top_prob, const int* seg_off, int nseg, int B, int C) {
-    seg_softmax_topk_kernel<<<B, 64, 0, s>>>(logits, probs, top_idx, top_prob, seg_off, nseg, C);
+    const int blocks = (B + SM_WAVES - 1) / SM_WAVES;
+    seg_softmax_topk_kernel<<<blocks, 64 * SM_WAVES, SM_WAVES * C * sizeof(float), s>>>(
+        logits, probs, top_idx, top_prob, seg_off, nseg, B, C);
 }
 
 }  // namespace clipvit

@@ -121,6 +121,8 @@ class VisionEngine:
         R = self.cfg.image_size
         if pixels.dim() != 4 or tuple(pixels.shape[1:]) != (3, R, R):
             raise ValueError(f"pixels must be [B, 3, {R}, {R}], got {tuple(pixels.shape)}")
+        if pixels.shape[0] == 0:
+            raise _lib.ClipVitError(_lib.E_INVALID, "empty batch")
         if pixels.dtype not in _PIX_DT:
             pixels = pixels.float()
         if pixels.device != self.device:

@@ -185,6 +185,7 @@ def make_clip_shim(visual_sd_by_name: dict, text_seed: int = 1234):
         return m, (lambda img: preprocess(img, geo.image_size))
 
     shim.load = load
+    shim.base_load = load
     shim.tokenize = lambda texts, context_length=77, truncate=False: _Tokens(
         [texts] if isinstance(texts, str) else texts)
     return shim

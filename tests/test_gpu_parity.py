@@ -132,6 +132,64 @@ def test_encode_image_unnormalised(gpu):
     assert torch.nn.functional.cosine_similarity(f, ref).min() > 0.9995
 
 
+def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
+    """The optional two-stream split (CLIPVIT_SPLIT_MIN) computes every image with the same
+    kernels and k-order, so its outputs equal the single-stream outputs bit for bit."""
+    cfg = C.VIT_B32
+    sd = synthetic_state_dict(cfg, 0)
+    T = _text(cfg.embed_dim, 437)
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    px = _pixels(96, 224, seed=21).to(gpu)
+    outs = []
+    for split in ("0", "64"):
+        monkeypatch.setenv("CLIPVIT_SPLIT_MIN", split)
+        eng = VisionEngine(cfg, 0, "fp16", max_batch=128)
+        eng.load_state_dict(sd)
+        eng.set_text_features(T.numpy(), seg)
+        o = eng.classify(px)
+        torch.cuda.synchronize()
+        outs.append((o.logits.clone(), o.top_idx.clone(), eng.encode_image(px).clone()))
+        eng.close()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[0][2], outs[1][2])
+
+
+def test_concurrent_host_threads(gpu):
+    """The reference calls encode_image from ThreadPoolExecutor(4) (main.py:345-346); the
+    handle must give every thread its own workspace and correct results."""
+    from concurrent.futures import ThreadPoolExecutor
+    cfg = C.VIT_B32
+    eng, ref_sd = _engine(cfg, "fp16", 0, max_batch=16)
+    pxs = [_pixels(3, 224, seed=100 + i).to(gpu) for i in range(8)]
+    serial = [eng.encode_image(p).clone() for p in pxs]
+    torch.cuda.synchronize()
+
+    def work(i):
+        s = torch.cuda.Stream(gpu)
+        with torch.cuda.stream(s):
+            out = eng.encode_image(pxs[i])
+        s.synchronize()
+        return out
+
+    with ThreadPoolExecutor(max_workers=4) as ex:
+        par = list(ex.map(work, range(8)))
+    for a, b in zip(serial, par):
+        assert torch.equal(a, b)
+
+
+def test_errors_are_reported_not_crashes(gpu):
+    from interior_amd import _lib
+    cfg = C.VIT_B32
+    eng, _ = _engine(cfg, "fp16", 0, max_batch=16)
+    with pytest.raises(_lib.ClipVitError):
+        eng.encode_image(torch.zeros(17, 3, 224, 224, device=gpu)[:0])  # B = 0
+    eng2 = VisionEngine(cfg, 0, "fp16", 4)
+    with pytest.raises(_lib.ClipVitError):
+        eng2.encode_image(torch.zeros(1, 3, 224, 224, device=gpu))     # weights not loaded
+    eng2.close()
+
+
 def test_full_batch_256_properties(gpu):
     """bs=256 (the metric's batch): every image equals its own bs=1 result bit-for-bit
     (per-image independence; rows never mix), and a sample of rows matches the oracle."""
