@@ -29,7 +29,7 @@ def to_pixels(img: Image.Image, n_px: int = 224) -> np.ndarray:
     img = img.resize((nw, nh), Image.BICUBIC)
     top, left = int(round((nh - n_px) / 2.0)), int(round((nw - n_px) / 2.0))
     img = img.crop((left, top, left + n_px, top + n_px)).convert("RGB")
-    a = np.asarray(img, dtype=np.float32) * (1.0 / 255.0)
+    a = np.asarray(img, dtype=np.float32) / 255.0  # ToTensor: div(255), then Normalize
     a = (a - MEAN) / STD
     return np.ascontiguousarray(a.transpose(2, 0, 1))
 

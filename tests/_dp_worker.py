@@ -1,0 +1,44 @@
+"""Worker body for tests/test_dp.py (importable in spawned children: registers the package)."""
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+import amd_pkg  # noqa: E402
+
+amd_pkg.load()
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from interior_amd import dp  # noqa: E402
+
+
+class FakeEngine:
+    """Stands in for VisionEngine on CPU: deterministic per-image logits."""
+
+    class Out:
+        def __init__(self, logits):
+            self.logits = logits
+
+    def classify(self, px, out=None):
+        return self.Out(px.reshape(px.shape[0], -1)[:, :5].sum(1, keepdim=True) * torch.arange(1., 8.))
+
+
+def worker(rank, world, port, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(0)
+        full = torch.randn(B, 3, 4, 4, generator=g)
+        a, b = dp.shard_bounds(B, world, rank)
+        logits, _ = dp.ShardedClassifier(FakeEngine()).classify_global(full[a:b], B)
+        ok = torch.equal(logits, FakeEngine().classify(full).logits)
+        eq = dp.allgather_rows(torch.full((3, 2), float(rank)))
+        ok &= torch.equal(eq, torch.cat([torch.full((3, 2), float(r)) for r in range(world)]))
+        q.put((rank, bool(ok)))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
