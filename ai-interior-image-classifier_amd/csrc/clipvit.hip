@@ -127,7 +127,9 @@ struct clipvit_handle {
     std::vector<Workspace*> pool;
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from tools/gemm_tune.py sweeps
     // on MI355X (profiles/); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
-    int var[5] = {8, 14, 13, 14, 14};
+    int var[5] = {8, 21, 21, 21, 21};
+    // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
+    int xcd[5] = {2, 1, 2, 1, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
 };
 
@@ -237,12 +239,16 @@ static void release_ws(clipvit_handle* h, Workspace* w) {
     w->used = false;
 }
 
+enum Role { R_QKV = 0, R_OUT, R_FC, R_PROJ, R_PATCH };
+
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
-                const float* bias, void* C, int M, int N, int K, int ldc, int variant) {
+                const float* bias, void* C, int M, int N, int K, int ldc, int role) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
+    a.xcd_n = h->xcd[role];
+    const int variant = h->var[role];
     // a tuned variant that does not tile this shape falls back to the shape-based choice
     if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -260,7 +266,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     int rc;
     if (prof) prof->mark(s, F_EMBED);
     launch_im2col(s, in_dtype, h->dt, pix, w->u, B, h->cfg.image_size, h->cfg.patch_size, h->Kp);
-    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, h->var[4]);
+    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, R_PATCH);
     if (rc) return rc;
     const LayerW& l0 = h->layers[0];
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
@@ -268,20 +274,20 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     if (prof) prof->mark(s, F_EMBED);
     for (int i = 0; i < h->cfg.layers; ++i) {
         const LayerW& ly = h->layers[i];
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, h->var[0])))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (prof) prof->mark(s, F_ATTN);
-        if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, h->var[1])))
+        if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT)))
             return rc;
         if (prof) prof->mark(s, F_OUT);
         launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
         if (prof) prof->mark(s, F_LN);
-        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, h->var[2])))
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC)))
             return rc;
         if (prof) prof->mark(s, F_FC);
-        if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, h->var[3])))
+        if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)))
             return rc;
         if (prof) prof->mark(s, F_PROJ);
         if (i + 1 < h->cfg.layers) {
@@ -391,6 +397,14 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;
+    }
+    if (const char* v = getenv("CLIPVIT_GEMM_XCD")) {
+        int k = 0;
+        for (const char* p = v; *p && k < 5; ++k) {
+            h->xcd[k] = atoi(p);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
     }
     if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
         int k = 0;
@@ -705,6 +719,8 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     GemmArgs a{};
     a.A = A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
+    a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
+    variant %= 100;
     const int e = epi == 0 ? EPI_F32 : epi == 1 ? EPI_F32GELU : EPI_RESID;
     const int rc = launch_gemm(s, dtype, e, a, variant);
     HIPCHK(hipFreeAsync(Wp, s));
@@ -731,6 +747,8 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.A = A; a.W = W; a.bias = bias; a.C = Cb;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.patch_g2 = 49; a.patch_ntok = 50;
+    a.xcd_n = variant / 100;
+    variant %= 100;
     const int e = epi;  // raw Epi enum
     int rc = launch_gemm(nullptr, dtype, e, a, variant);
     hipEvent_t t0, t1;

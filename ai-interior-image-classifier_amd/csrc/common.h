@@ -80,7 +80,45 @@ struct GemmArgs {
     void* C;           // output, row stride ldc (elements)
     int M, N, K, ldc;
     int patch_g2, patch_ntok;  // EPI_PATCH row remap: m -> (m / g2) * ntok + 1 + m % g2
+    int xcd_n;  // tile->XCD partition: 2 = 4 M-bands x 2 N-halves per XCD group (else 1-D)
 };
+
+// Map a launch-order block id to its (m-tile, n-tile). Blocks b, b+8, ... are observed to
+// share an XCD (speed only, never correctness). With xn == 2 the 8 XCD groups form a 4 x 2
+// grid over (M, N): each group streams its M-band's A panels once and keeps HALF of W in its
+// 4 MB L2; tiles inside a group run M-major. Returns false for padding blocks.
+__device__ __forceinline__ bool tile_of_block(int bid, int nM, int nN, int xn, int& mt, int& nt) {
+    if (xn == 2 && (nN & 1) == 0) {
+        const int x = bid & 7, j = bid >> 3;
+        const int xm = x >> 1, xh = x & 1;
+        const int m_lo = (nM * xm) >> 2, m_hi = (nM * (xm + 1)) >> 2;
+        const int n_lo = xh * (nN >> 1), nr = nN >> 1;
+        if (j >= (m_hi - m_lo) * nr) return false;
+        mt = m_lo + j / nr;
+        nt = n_lo + j % nr;
+        return true;
+    }
+    const int nwg = nM * nN;  // bijective 1-D remap: each group takes a contiguous range
+    if (bid >= nwg) return false;
+    const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+    mt = t / nN;
+    nt = t % nN;
+    return true;
+}
+
+// Grid size matching tile_of_block: 8 x (largest group) for the 2-D partition.
+inline int grid_for(int nM, int nN, int xn) {
+    if (xn == 2 && (nN & 1) == 0) {
+        int mx = 0;
+        for (int xm = 0; xm < 4; ++xm) {
+            const int rows = ((nM * (xm + 1)) >> 2) - ((nM * xm) >> 2);
+            mx = rows > mx ? rows : mx;
+        }
+        return 8 * mx * (nN >> 1);
+    }
+    return nM * nN;
+}
 
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)

@@ -22,6 +22,7 @@
 //  * v_mfma_f32_16x16x32_{bf16,f16}, fp32 accumulation; epilogue adds bias, QuickGELU
 //    (x * sigmoid(1.702 x), CLIP's activation) or the fp32 residual add;
 //  * bijective XCD-aware block remap: consecutive logical tiles (same A panel) share an XCD L2.
+#include <algorithm>
 #include "common.h"
 
 namespace clipvit {
@@ -199,9 +200,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     constexpr int FM = TM / 16, FN = TN / 16;
     static_assert(TN % 64 == 0 && TM % 16 == 0, "wave tile");
     constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
-    constexpr int LA = A_BYTES / (NT * 16), LW = W_BYTES / (NT * 16);
-    static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "staging rounds");
-    constexpr int LPT = LA + LW;  // glds per thread per tile
+    // staging rounds; a last partial round (e.g. BM = 160) is issued by whole waves only, which
+    // makes per-wave load counts differ -> allowed only with NS = 2 (waits are vmcnt(0) there)
+    constexpr int LA = (A_BYTES + NT * 16 - 1) / (NT * 16), LW = (W_BYTES + NT * 16 - 1) / (NT * 16);
+    constexpr bool PARTIAL = LA * NT * 16 != A_BYTES || LW * NT * 16 != W_BYTES;
+    static_assert(!PARTIAL || NS == 2, "partial staging rounds need NS == 2");
+    static_assert(A_BYTES % 1024 == 0 && W_BYTES % 1024 == 0, "whole-wave staging pieces");
+    constexpr int LPT = LA + LW;  // glds per thread per tile (upper bound when PARTIAL)
     constexpr int STAGE = A_BYTES + W_BYTES;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
 
@@ -209,13 +214,9 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int nN = a.N / BN;
-    const int nwg = gridDim.x;
-    int bid = blockIdx.x;
-    {
-        const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
-        bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
-    }
-    const int m0 = (bid / nN) * BM, n0 = (bid % nN) * BN;
+    int mt, nt;
+    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, nN, a.xcd_n, mt, nt)) return;
+    const int m0 = mt * BM, n0 = nt * BN;
 
     const unsigned char* Ab = (const unsigned char*)a.A;
     const unsigned char* Wb = (const unsigned char*)a.W;
@@ -240,9 +241,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = (size_t)kt * 128;
 #pragma unroll
-        for (int r = 0; r < LA; ++r) glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
+        for (int r = 0; r < LA; ++r)
+            if (r * NT * 16 + wave * 1024 < A_BYTES)  // wave-uniform
+                glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
 #pragma unroll
-        for (int r = 0; r < LW; ++r) glds16(Wb + wsrc[r] + kofs, sW + r * NT * 16 + wave * 1024);
+        for (int r = 0; r < LW; ++r)
+            if (r * NT * 16 + wave * 1024 < W_BYTES)
+                glds16(Wb + wsrc[r] + kofs, sW + r * NT * 16 + wave * 1024);
     };
 
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
@@ -575,7 +580,7 @@ static void launch_pp(hipStream_t s, int epi, const GemmArgs& a) {
 
 template <typename T, int BM, int BN, int WM, int WN, int NS>
 static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
-    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+    const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
     dim3 grid(nwg), block(64 * WM * WN);
     switch (epi) {
         case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE><<<grid, block, 0, s>>>(a); break;
@@ -584,6 +589,225 @@ static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
         case EPI_PATCH: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
         case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
         case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused epilogue for one wave's TM x TN block (shared by the persistent kernel).
+template <typename T, int EPI, int FM, int FN>
+__device__ __forceinline__ void epilogue_wave(const GemmArgs& a, f32x4 (&acc)[FN][FM], int mbase,
+                                              int nbase, int lane) {
+    const int g = lane >> 4, lrow = lane & 15;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = mbase + fm * 16 + lrow;
+        if (m >= a.M) continue;
+#pragma unroll
+        for (int q = 0; q < FN / 4; ++q) {
+            const int n = nbase + q * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
+            if constexpr (EPI != EPI_PATCH) {
+                if (a.bias) {
+                    const float4* b4 = (const float4*)(a.bias + n);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 bb = b4[i];
+                        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                    }
+                }
+            }
+            if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+            }
+            if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+                dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                    pack2<T>(v[6], v[7]));
+                dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                    pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+            } else if constexpr (EPI == EPI_RESID) {
+                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float4 o = dst[i];
+                    o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                    dst[i] = o;
+                }
+            } else {
+                size_t row = (size_t)m;
+                if constexpr (EPI == EPI_PATCH)
+                    row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
+                float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent pipelined GEMM: grid = min(#tiles, #CUs); block b owns tiles b, b + G, b + 2G, ...
+// and runs ONE continuous 2-stage LDS ring over the concatenated k-steps of all its tiles, so
+// the first k-tiles of tile i+1 are loaded (and its first fragments read) while tile i's last
+// MFMAs and its epilogue run: the per-tile load latency of a 768-deep K is paid once per block.
+template <typename T, int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM* WN) void gemm_persist_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(TN % 64 == 0 && TM % 16 == 0, "wave tile");
+    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
+    constexpr int LA = (A_BYTES + NT * 16 - 1) / (NT * 16), LW = (W_BYTES + NT * 16 - 1) / (NT * 16);
+    static_assert(A_BYTES % 1024 == 0 && W_BYTES % 1024 == 0, "whole-wave staging pieces");
+    constexpr int STAGE = A_BYTES + W_BYTES;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int nN = a.N / BN;
+    const int ntiles = nN * ((a.M + BM - 1) / BM);
+    const int G = gridDim.x, b = blockIdx.x;
+    const int my_tiles = (ntiles - b + G - 1) / G;
+    const int nk = a.K >> 6;
+    const int S = my_tiles * nk;
+
+    auto tile_origin = [&](int i, int& m0, int& n0) {  // i-th tile of this block
+        int t = b + i * G;
+        const int q = ntiles >> 3, r = ntiles & 7, x = t & 7;  // bijective XCD remap
+        t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (t >> 3);
+        m0 = (t / nN) * BM;
+        n0 = (t % nN) * BN;
+    };
+
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K * 2;
+    const int mlast = a.M - 1;
+    int arow[LA], acol[LA], wrow[LW], wcol[LW];
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        arow[r] = p >> 7;
+        acol[r] = (((p >> 4) & 7) ^ (arow[r] & 7)) * 16;
+    }
+#pragma unroll
+    for (int r = 0; r < LW; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        wrow[r] = p >> 7;
+        wcol[r] = (((p >> 4) & 7) ^ (wrow[r] & 7)) * 16;
+    }
+    auto stage = [&](int buf, int step) {
+        int m0, n0;
+        tile_origin(step / nk, m0, n0);
+        const size_t kofs = (size_t)(step % nk) * 128;
+        unsigned char* sA = smem + buf * STAGE;
+        unsigned char* sW = sA + A_BYTES;
+#pragma unroll
+        for (int r = 0; r < LA; ++r)
+            if (r * NT * 16 + wave * 1024 < A_BYTES)
+                glds16(Ab + (size_t)min(m0 + arow[r], mlast) * ldb + kofs + acol[r],
+                       sA + r * NT * 16 + wave * 1024);
+#pragma unroll
+        for (int r = 0; r < LW; ++r)
+            if (r * NT * 16 + wave * 1024 < W_BYTES)
+                glds16(Wb + (size_t)(n0 + wrow[r]) * ldb + kofs + wcol[r], sW + r * NT * 16 + wave * 1024);
+    };
+
+    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
+    const int aoff = (wm * TM + lrow) * 128, woff = A_BYTES + (wn * TN + lrow) * 128;
+    auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
+        const unsigned char* base = smem + buf * STAGE;
+        const int c = (((s << 2) | lg) ^ lsw) << 4;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + c);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + c);
+    };
+
+    f32x4 acc[FN][FM];
+    auto zero = [&]() {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+    };
+    auto finish_tile = [&](int step) {
+        int m0, n0;
+        tile_origin(step / nk, m0, n0);
+        epilogue_wave<T, EPI, FM, FN>(a, acc, m0 + wm * TM, n0 + wn * TN, lane);
+        zero();
+    };
+
+    zero();
+    if (S == 0) return;
+    stage(0, 0);
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (S > 1) stage(1, 1);
+    vec8 a0[FM], w0[FN], a1[FM], w1[FN];
+    load_frags(0, 0, a0, w0);
+    for (int s = 0; s < S - 1; ++s) {
+        const int cur = s & 1;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        load_frags(cur, 1, a1, w1);
+        mfmas(a0, w0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // stage `cur` fully read
+        vm_wait<0>();                        // step s+1 landed (own loads; also epilogue stores)
+        __builtin_amdgcn_s_barrier();
+        if (s + 2 < S) stage(cur, s + 2);
+        load_frags(cur ^ 1, 0, a0, w0);
+        mfmas(a1, w1);
+        if ((s + 1) % nk == 0) finish_tile(s);  // next step starts a new tile
+    }
+    {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        load_frags((S - 1) & 1, 1, a1, w1);
+        mfmas(a0, w0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        mfmas(a1, w1);
+        finish_tile(S - 1);
+    }
+}
+
+static int g_num_cus = 0;
+static int num_cus() {
+    if (!g_num_cus) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+            g_num_cus = n;
+        else
+            g_num_cus = 256;
+    }
+    return g_num_cus;
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+static void launch_persist(hipStream_t s, int epi, const GemmArgs& a) {
+    const int ntiles = (a.N / BN) * ((a.M + BM - 1) / BM);
+    const int grid = std::min(ntiles, num_cus());
+    dim3 block(64 * WM * WN);
+    switch (epi) {
+        case EPI_STORE: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+        case EPI_PATCH: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32GELU: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
     }
 }
 
@@ -674,6 +898,35 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         case 15:
             if (a.N % 256 || a.K % 32) return -1;
             launch_pp<T>(s, epi, a);
+            return 0;
+        case 21:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 160, 256, 2, 4, 2>(s, epi, a);
+            return 0;
+        case 22:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 160, 128, 2, 2, 2>(s, epi, a);
+            return 0;
+        case 23:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 224, 256, 2, 4, 2>(s, epi, a);
+            return 0;
+        // ---- persistent ring variants ----
+        case 24:
+            if (a.N % 256) return -1;
+            launch_persist<T, 160, 256, 2, 4>(s, epi, a);
+            return 0;
+        case 25:
+            if (a.N % 256) return -1;
+            launch_persist<T, 256, 256, 2, 4>(s, epi, a);
+            return 0;
+        case 26:
+            if (a.N % 128) return -1;
+            launch_persist<T, 128, 128, 4, 2>(s, epi, a);
+            return 0;
+        case 27:
+            if (a.N % 256) return -1;
+            launch_persist<T, 128, 256, 2, 4>(s, epi, a);
             return 0;
         case 16: case 17: case 18: case 19: case 20: {  // ablations (timing only)
             if (a.N % 256 || a.K % 32) return -1;

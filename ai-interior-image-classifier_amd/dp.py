@@ -33,9 +33,14 @@ def allgather_rows(local: torch.Tensor, group=None) -> torch.Tensor:
     world = dist.get_world_size(group)
     if world == 1:
         return local
+    local = local.contiguous()
+    if dist.get_backend(group) == "gloo":  # gloo has no all_gather_into_tensor
+        parts = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(parts, local, group=group)
+        return torch.cat(parts, dim=0)
     out = torch.empty((world * local.shape[0], *local.shape[1:]), dtype=local.dtype,
                       device=local.device)
-    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    dist.all_gather_into_tensor(out, local, group=group)  # RCCL over xGMI
     return out
 
 

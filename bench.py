@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-iters", type=int, default=5)
+    p.add_argument("--share-gpu", action="store_true",
+                   help="all ranks on cuda:0 with gloo (multi-rank rehearsal on one GPU)")
     return p.parse_args()
 
 
@@ -102,10 +104,16 @@ def load_traffic(cfg_name: str, batch: int):
 def main():
     a = parse()
     rank, local_rank, world = env_rank()
+    # --share-gpu: every rank on cuda:0 (rehearsal of the N-rank code path on a 1-GPU box;
+    # RCCL refuses two ranks on one device, so that mode uses gloo for the all-gather)
+    gpu_index = 0 if a.share_gpu else local_rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu_index)
+        if a.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu_index))
+    dev = torch.device("cuda", gpu_index)
     torch.cuda.set_device(dev)
     cfg = C.get_config(a.model)
 

@@ -143,7 +143,10 @@ int clipvit_abi_version(void);
  * W_dev: fp32 [N,K] natural row order (packed to `dtype` internally, as clipvit_load_weights
  * does); bias fp32 [N] or NULL; C fp32 [M,N]. epi: 0 = store, 1 = QuickGELU then store,
  * 2 = accumulate into C (residual add). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
- * N % 256 for variant 3). variant: 0 auto, 1 128x128, 2 256x128, 3 256x256, 4 64x64. */
+ * N % 256 for variant 3). variant % 100 selects the tile kernel (0 auto; the table in
+ * csrc/gemm.hip pick/launch_gemm); variant / 100 the block->XCD mapping
+ * (0/1 = 1-D bijective remap, 2 = 4x2 (M-band, N-half) partition; pipelined variants only).
+ * The same encoding applies to clipvit_gemm_bench. */
 int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi,
                       int variant);

@@ -26,12 +26,19 @@ def _ref_gemm(A, W, bias, epi, C0=None):
     return ref
 
 
+# variant = 100 * xcd_partition + tile kernel (include/clipvit.h); 2xx = 4x2 XCD tile partition
+VARIANTS = list(range(1, 16)) + [21, 22, 23, 24, 25, 26, 27, 208, 213, 221, 222]
+N128 = (1, 2, 6, 7, 10, 11, 12, 13, 22, 26)
+N256 = (3, 5, 8, 9, 14, 15, 21, 23, 24, 25, 27)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("variant", list(range(1, 16)))
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("M,N,K", [(12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
                                    (700, 768, 3072), (64, 256, 64)])
 def test_gemm_shapes(gpu, dtype, variant, M, N, K):
-    if (variant in (1, 2, 6, 7, 10, 11, 12, 13) and N % 128) or (variant in (3, 5, 8, 9, 14, 15) and N % 256):
+    v = variant % 100
+    if (v in N128 and N % 128) or (v in N256 and N % 256):
         pytest.skip("tile does not divide N")
     g = torch.Generator(device=gpu).manual_seed(M + N + K)
     A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
@@ -63,7 +70,7 @@ def test_gemm_asymmetric_identity(gpu):
     K = N = 256
     A = torch.eye(K, device=gpu).to(torch.bfloat16)
     W = (torch.arange(N * K, device=gpu, dtype=torch.float32).reshape(N, K) % 251) / 8.0
-    for variant in range(1, 16):
+    for variant in VARIANTS:
         C = E.gemm_test(A, W, None, epi=0, variant=variant)
         assert torch.equal(C, W.to(torch.bfloat16).float().t()), variant
 

@@ -1,0 +1,108 @@
+"""Turn a tools/profile_round.sh output directory into committed summaries under profiles/.
+
+    python tools/summarize_profiles.py gpurun_out/prof r01
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim), profiles/<tag>_summary.md
+(per-kernel-role averages, MFMA TFLOP/s, PMC bytes per launch) and updates
+profiles/pmc_traffic.json (read by bench.py's roofline.traffic).
+
+Kernel roles are assigned from the dispatch order of one forward (per layer: qkv GEMM,
+attention, out GEMM, layernorm, fc GEMM, proj GEMM, layernorm), which is how out- and
+proj-GEMM dispatches of the same template instance are told apart.
+"""
+import csv
+import json
+import shutil
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def gemm_like(name):
+    return "gemm" in name
+
+
+def roles_for_trace(rows):
+    """Assign a role to every dispatch of the encoder forward, by order."""
+    out = []
+    layer_seq = ["qkv", "attention", "out", "ln2", "fc", "proj", "ln1"]
+    pos = None
+    for r in rows:
+        n = r["Kernel_Name"]
+        if "im2col" in n:
+            out.append("im2col"); pos = "patch"; continue
+        if pos == "patch" and gemm_like(n):
+            out.append("patch_gemm"); pos = 0; continue
+        if "embed_ln" in n:
+            out.append("embed_ln"); pos = 0; continue
+        if "cls_ln_proj" in n:
+            out.append("head_proj"); pos = None; continue
+        if "logits_kernel" in n:
+            out.append("head_logits"); continue
+        if "seg_softmax" in n:
+            out.append("head_softmax"); continue
+        if isinstance(pos, int) and (gemm_like(n) or "attention" in n or "layernorm" in n):
+            out.append(layer_seq[pos % 7]); pos += 1; continue
+        out.append("other")
+    return out
+
+
+def load_rows(path):
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r.get("Start_Timestamp") or r.get("Dispatch_Id") or 0))
+    return rows
+
+
+def main():
+    src, tag = Path(sys.argv[1]), sys.argv[2]
+    prof = ROOT / "profiles"
+    prof.mkdir(exist_ok=True)
+    kt = next((src / "kt").rglob("*kernel_stats.csv"))
+    shutil.copyfile(kt, prof / f"{tag}_kernel_stats.csv")
+    trace = load_rows(next((src / "kt").rglob("*kernel_trace.csv")))
+    roles = roles_for_trace(trace)
+    dur = defaultdict(list)
+    for r, role in zip(trace, roles):
+        dur[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+
+    def pmc(kind):
+        f = next((src / kind).rglob("*counter_collection.csv"))
+        rows = [r for r in load_rows(f)]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        rr = roles_for_trace(rows)
+        acc = defaultdict(list)
+        for r, role in zip(rows, rr):
+            acc[role].append(float(r["Counter_Value"]))
+        return acc
+
+    fetch, write = pmc("fetch"), pmc("write")
+    M, D = 256 * 50, 768
+    flops = {"qkv": 2 * M * D * 3 * D, "out": 2 * M * D * D, "fc": 2 * M * D * 4 * D,
+             "proj": 2 * M * D * 4 * D, "patch_gemm": 2 * 256 * 49 * 3072 * D}
+    lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16)", "",
+             "| role | dispatches | avg us | TFLOP/s | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) |",
+             "|---|---|---|---|---|---|"]
+    traffic = {}
+    for role in sorted(dur, key=lambda k: -sum(dur[k])):
+        d = dur[role]
+        avg = sum(d) / len(d)
+        tf = f"{flops[role] / (avg * 1e-6) / 1e12:.0f}" if role in flops else ""
+        fb = 2 * sum(fetch[role]) / len(fetch[role]) * 1024 / 1e6 if fetch.get(role) else float("nan")
+        wb = sum(write[role]) / len(write[role]) * 1024 / 1e6 if write.get(role) else float("nan")
+        traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6}
+        lines.append(f"| {role} | {len(d)} | {avg:.1f} | {tf} | {fb:.1f} | {wb:.1f} |")
+    (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
+    mlp = [traffic[r] for r in ("fc", "proj") if r in traffic]
+    entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
+             "mlp_gemm_avg_us": sum(t["avg_us"] for t in mlp) / len(mlp), "source": f"profiles/{tag}_summary.md",
+             "note": "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reports half of wide streaming reads); Infinity-Cache hits are included by the counters"}
+    pj = prof / "pmc_traffic.json"
+    data = json.loads(pj.read_text()) if pj.exists() else {}
+    data["ViT-B/32|256"] = entry
+    pj.write_text(json.dumps(data, indent=1))
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
