@@ -127,9 +127,9 @@ struct clipvit_handle {
     std::vector<Workspace*> pool;
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from tools/gemm_tune.py sweeps
     // on MI355X (profiles/); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
-    int var[5] = {8, 21, 21, 21, 21};
+    int var[5] = {8, 21, 13, 21, 21};
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
-    int xcd[5] = {2, 1, 2, 1, 1};
+    int xcd[5] = {2, 2, 2, 2, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
 };
 
@@ -721,8 +721,22 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
-    const int e = epi == 0 ? EPI_F32 : epi == 1 ? EPI_F32GELU : EPI_RESID;
-    const int rc = launch_gemm(s, dtype, e, a, variant);
+    int rc;
+    if (variant >= 30 && variant < 40) {  // 16-bit-output kernels: run, then widen to fp32
+        if (epi == 2) {
+            hipFreeAsync(Wp, s);
+            FAIL(CLIPVIT_E_INVALID, "variant has no residual epilogue");
+        }
+        void* C16 = nullptr;
+        HIPCHK(hipMallocAsync(&C16, (size_t)M * N * 2, s));
+        a.C = C16;
+        rc = launch_gemm(s, dtype, epi == 0 ? EPI_STORE : EPI_GELU, a, variant);
+        if (!rc) launch_widen16(s, dtype, C16, C_dev, (size_t)M * N);
+        HIPCHK(hipFreeAsync(C16, s));
+    } else {
+        const int e = epi == 0 ? EPI_F32 : epi == 1 ? EPI_F32GELU : EPI_RESID;
+        rc = launch_gemm(s, dtype, e, a, variant);
+    }
     HIPCHK(hipFreeAsync(Wp, s));
     if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
     HIPCHK(hipGetLastError());

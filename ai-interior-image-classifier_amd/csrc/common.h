@@ -9,6 +9,21 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// 16-byte global stores; NT = non-temporal (streamed past L2 so a GEMM's output does not
+// evict the operand panels the other tiles still re-read).
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)p);
+    else *(uint4*)p = v;
+}
+template <bool NT>
+__device__ __forceinline__ void st16f(void* p, float4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(f32x4v{v.x, v.y, v.z, v.w}, (f32x4v*)p);
+    else *(float4*)p = v;
+}
 
 #define LDS_AS __attribute__((address_space(3)))
 #define GLB_AS __attribute__((address_space(1)))
@@ -71,6 +86,7 @@ enum Epi {
     EPI_PATCH = 3,   // C (f32) [remapped token row] = acc          (conv1 has no bias)
     EPI_F32 = 4,     // C (f32) = acc + bias                         (tests)
     EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
+    EPI_DISCARD = 6, // no stores (epilogue-cost ablation; timing only, pipelined kernel)
 };
 
 struct GemmArgs {
@@ -108,7 +124,7 @@ __device__ __forceinline__ bool tile_of_block(int bid, int nM, int nN, int xn, i
 }
 
 // Grid size matching tile_of_block: 8 x (largest group) for the 2-D partition.
-inline int grid_for(int nM, int nN, int xn) {
+__host__ __device__ inline int grid_for(int nM, int nN, int xn) {
     if (xn == 2 && (nN & 1) == 0) {
         int mx = 0;
         for (int xm = 0; xm < 4; ++xm) {
@@ -123,6 +139,8 @@ inline int grid_for(int nM, int nN, int xn) {
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
+
+void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n);
 
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H);
 

@@ -139,7 +139,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_nt_kernel(GemmArgs a) {
             }
             if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
@@ -192,7 +192,7 @@ __device__ __forceinline__ void wait_tile(int r) {
     vm_wait<0>();
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool NTS = false>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
@@ -349,22 +349,27 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
             }
             if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
-                dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
-                                    pack2<T>(v[6], v[7]));
-                dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
-                                    pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+                st16<NTS>(dst, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                          pack2<T>(v[6], v[7])));
+                st16<NTS>(dst + 1, make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                              pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
             } else if constexpr (EPI == EPI_RESID) {
                 float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     float4 o = dst[i];
                     o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
-                    dst[i] = o;
+                    st16f<NTS>(dst + i, o);
                 }
+            } else if constexpr (EPI == EPI_DISCARD) {
+                float t = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) t += v[i];
+                if (t == 1.2345e-30f) ((float*)a.C)[0] = t;  // never taken; keeps the MFMAs live
             } else {
                 size_t row = (size_t)m;
                 if constexpr (EPI == EPI_PATCH)
@@ -536,7 +541,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
         }
         if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+            for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
         }
         if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
             uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
@@ -578,10 +583,19 @@ static void launch_pp(hipStream_t s, int epi, const GemmArgs& a) {
     }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS>
+template <typename T, int BM, int BN, int WM, int WN, int NS, bool NTS = false>
 static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
     dim3 grid(nwg), block(64 * WM * WN);
+    if constexpr (NTS) {  // non-temporal-store builds: production epilogues only
+        switch (epi) {
+            case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE, true><<<grid, block, 0, s>>>(a); break;
+            case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU, true><<<grid, block, 0, s>>>(a); break;
+            case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID, true><<<grid, block, 0, s>>>(a); break;
+            default: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        }
+        return;
+    }
     switch (epi) {
         case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE><<<grid, block, 0, s>>>(a); break;
         case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU><<<grid, block, 0, s>>>(a); break;
@@ -589,7 +603,20 @@ static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
         case EPI_PATCH: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
         case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
         case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_DISCARD: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_DISCARD><<<grid, block, 0, s>>>(a); break;
     }
+}
+
+// 16-bit -> fp32 copy (test entry for the 16-bit-output kernels)
+template <typename T>
+__global__ void widen16_kernel(const u16* src, float* dst, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = T::to_f32(src[i]);
+}
+void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n) {
+    const unsigned g = (unsigned)((n + 255) / 256);
+    if (dtype == 2) widen16_kernel<F16><<<g, 256, 0, s>>>((const u16*)src, dst, n);
+    else widen16_kernel<BF16><<<g, 256, 0, s>>>((const u16*)src, dst, n);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -622,7 +649,7 @@ __device__ __forceinline__ void epilogue_wave(const GemmArgs& a, f32x4 (&acc)[FN
             }
             if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] = v[i] / (1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
@@ -783,6 +810,260 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_persist_kernel(GemmArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent GEMM with a DEFERRED epilogue (16-bit outputs: EPI_STORE / EPI_GELU).
+//
+// Why: in a one-tile-per-block GEMM every CU reaches its epilogue at the same moment, so the
+// whole output (78.6 MB for c_fc at bs=256) is written in a chip-wide burst while the MFMAs
+// idle — measured on MI355X as 25-30 % of c_fc / qkv time (tools/gemm_tune.py --epi 6).
+// Here a block owns tiles b, b+G, ... and runs one continuous 2-stage LDS ring over all
+// their k-steps (as gemm_persist_kernel). At a tile's end the waves convert their
+// accumulators (bias, QuickGELU, 16-bit) into an LDS stash [BM][BN] and go straight on with
+// the next tile; the stash is written to HBM during the next tile's first 8 k-steps, one
+// fully coalesced 16-B-per-lane global_store per wave per k-step, so the stores overlap MFMAs.
+//
+// Stash: row pitch BN*2 B, 16-B chunk c of row r at chunk c ^ (r & 7): the epilogue's
+// ds_write_b128 (8 rows x one chunk per 8-lane group) and the drain's ds_read_b128 (one row
+// per 32 lanes) are both conflict-free. Per k-step (after the barrier): stage(k+2), store of
+// the chunk read one step earlier, fragment reads, drain read of the next chunk. vmcnt is
+// counted by hand: the glds of step k+1 are waited with the one younger store left in flight.
+// Needs nk >= 9 (the 8 drain reads of a stash finish before the next stash is written).
+template <typename T, int BM, int BN, int WM, int WN, int EPI, int ABL = 0, bool NTS = false>
+__global__ __launch_bounds__(64 * WM* WN) void gemm_defer_kernel(GemmArgs a) {
+    // ABL (timing-only ablations, output wrong): bit0 no global stores, bit1 no stash writes
+    typedef typename T::vec8 vec8;
+    static_assert(EPI == EPI_STORE || EPI == EPI_GELU, "16-bit outputs only");
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(TN % 64 == 0 && TM % 16 == 0, "wave tile");
+    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
+    constexpr int LA = A_BYTES / (NT * 16), LW = W_BYTES / (NT * 16);
+    static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "whole staging rounds");
+    constexpr int STAGE = A_BYTES + W_BYTES;
+    constexpr int ROWB = BN * 2, CPR = ROWB / 16;     // stash row bytes, 16-B chunks per row
+    constexpr int STASH = BM * ROWB;
+    constexpr int DRAIN = STASH / (NT * 16);          // drain pieces per thread per tile
+    static_assert(DRAIN * NT * 16 == STASH && DRAIN <= 8 && NT % CPR == 0, "drain shape");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + STASH];
+    unsigned char* const stash = smem + 2 * STAGE;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int nN = a.N / BN, nM = (a.M + BM - 1) / BM;
+    const int G = gridDim.x, b = blockIdx.x;
+    const int V = grid_for(nM, nN, a.xcd_n);
+    int my_tiles = 0;
+    for (int mt, nt; b + my_tiles * G < V && tile_of_block(b + my_tiles * G, nM, nN, a.xcd_n, mt, nt);)
+        ++my_tiles;
+    const int nk = a.K >> 6;
+    const int S = my_tiles * nk;
+    if (S == 0) return;
+
+    auto tile_origin = [&](int i, int& m0, int& n0) {
+        int mt = 0, nt = 0;
+        tile_of_block(b + i * G, nM, nN, a.xcd_n, mt, nt);
+        m0 = mt * BM;
+        n0 = nt * BN;
+    };
+
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K * 2;
+    const int mlast = a.M - 1;
+    int arow[LA], acol[LA], wrow[LW], wcol[LW];
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        arow[r] = p >> 7;
+        acol[r] = (((p >> 4) & 7) ^ (arow[r] & 7)) * 16;
+    }
+#pragma unroll
+    for (int r = 0; r < LW; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        wrow[r] = p >> 7;
+        wcol[r] = (((p >> 4) & 7) ^ (wrow[r] & 7)) * 16;
+    }
+    auto stage = [&](int buf, int step) {
+        int m0, n0;
+        tile_origin(step / nk, m0, n0);
+        const size_t kofs = (size_t)(step % nk) * 128;
+        unsigned char* sA = smem + buf * STAGE;
+        unsigned char* sW = sA + A_BYTES;
+#pragma unroll
+        for (int r = 0; r < LA; ++r)
+            glds16(Ab + (size_t)min(m0 + arow[r], mlast) * ldb + kofs + acol[r], sA + r * NT * 16 + wave * 1024);
+#pragma unroll
+        for (int r = 0; r < LW; ++r)
+            glds16(Wb + (size_t)(n0 + wrow[r]) * ldb + kofs + wcol[r], sW + r * NT * 16 + wave * 1024);
+    };
+
+    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
+    const int aoff = (wm * TM + lrow) * 128, woff = A_BYTES + (wn * TN + lrow) * 128;
+    auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
+        const unsigned char* base = smem + buf * STAGE;
+        const int c = (((s << 2) | lg) ^ lsw) << 4;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + c);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + c);
+    };
+
+    f32x4 acc[FN][FM];
+    auto zero = [&]() {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+            for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    constexpr int NFR = FM + FN, NMF = FM * FN;
+    static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < NFR; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF - NFR, 0);
+    };
+    auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+    };
+
+    // accumulators (+bias, QuickGELU) -> 16-bit stash
+    // This lane's 16 bias values per 64-column group of the tile, loaded at the tile end. The
+    // tile's last k-step issues its DMA only after the stash write, so the vmcnt(0) the
+    // compiler puts before the first use of `bq` waits for these loads only.
+    float4 bq[FN / 4][4];
+    auto bias_load = [&](int n0) {
+#pragma unroll
+        for (int q = 0; q < FN / 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bq[q][i] = ((const float4*)(a.bias + n0 + wn * TN + q * 64 + 16 * lg))[i];
+    };
+    auto stash_write = [&](int n0) {
+        if (ABL & 2) return;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int r = wm * TM + fm * 16 + lrow;
+#pragma unroll
+            for (int q = 0; q < FN / 4; ++q) {
+                const int cl = wn * TN + q * 64 + 16 * lg;  // local column of this lane's 16
+                float v[16];
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) v[4 * f + i] = acc[4 * q + f][fm][i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    v[4 * i] += bq[q][i].x; v[4 * i + 1] += bq[q][i].y;
+                    v[4 * i + 2] += bq[q][i].z; v[4 * i + 3] += bq[q][i].w;
+                }
+                if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                }
+                const int c0 = cl >> 3, x = r & 7;
+                // inline asm: a compiler-visible ds_write after an LDS-DMA gets a vmcnt(0)
+                // (ordering against the DMA, which never targets the stash); completion is
+                // covered by the lgkmcnt(0) before the next barrier
+                const u32x4 lo = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+                const u32x4 hi = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
+                const unsigned p0 = (unsigned)(uintptr_t)(stash + r * ROWB + ((c0 ^ x) << 4));
+                const unsigned p1 = (unsigned)(uintptr_t)(stash + r * ROWB + (((c0 + 1) ^ x) << 4));
+                asm volatile("ds_write_b128 %0, %1" : : "v"(p0), "v"(lo) : "memory");
+                asm volatile("ds_write_b128 %0, %1" : : "v"(p1), "v"(hi) : "memory");
+            }
+        }
+    };
+    int dm0 = 0, dn0 = 0;  // origin of the stashed tile
+    auto drain_read = [&](int i) -> uint4 {
+        const int L = i * NT + tid, r = L / CPR, c = L % CPR;
+        return *(const uint4*)(stash + r * ROWB + ((c ^ (r & 7)) << 4));
+    };
+    // In-loop drain read as inline asm: a compiler-visible LDS load after an LDS-DMA gets an
+    // s_waitcnt vmcnt(0) (the compiler cannot tell the stash from the ring), which would wait
+    // for the DMA just issued. The explicit lgkmcnt(0) at the top of the next step (before
+    // the store that consumes `d`) covers the read.
+    auto drain_read_async = [&](int i, uint4& d) {
+        const int L = i * NT + tid, r = L / CPR, c = L % CPR;
+        const unsigned addr = (unsigned)(uintptr_t)(stash + r * ROWB + ((c ^ (r & 7)) << 4));
+        asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(addr) : "memory");
+    };
+    auto drain_store = [&](int i, uint4 d) {
+        const int L = i * NT + tid, r = L / CPR, c = L % CPR;
+        if (ABL & 1) return;
+        if (dm0 + r < a.M) st16<NTS>((u16*)a.C + (size_t)(dm0 + r) * a.ldc + dn0 + c * 8, d);
+    };
+
+    zero();
+    stage(0, 0);
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (S > 1) stage(1, 1);
+    vec8 a0[FM], w0[FN], a1[FM], w1[FN];
+    load_frags(0, 0, a0, w0);
+    int dcnt = DRAIN;      // drain pieces of the stash already read (DRAIN: nothing pending)
+    bool dpend = false;    // a piece read last step awaits its store
+    bool stored = false;   // a store was issued after the most recent stage()
+    uint4 d = make_uint4(0, 0, 0, 0);
+    for (int s = 0; s < S - 1; ++s) {
+        const int cur = s & 1;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // a0/w0 (and the drain piece) landed
+        load_frags(cur, 1, a1, w1);
+        mfmas(a0, w0);
+        interleave();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // stage `cur` fully read
+        if (stored) vm_wait<1>(); else vm_wait<0>();  // step s+1's glds landed
+        __builtin_amdgcn_s_barrier();
+        const bool tile_end = (s + 1) % nk == 0;
+        if (!tile_end && s + 2 < S) stage(cur, s + 2);
+        // the previous piece's store is the youngest vm op when the next step waits for this DMA
+        stored = dpend;
+        if (dpend) drain_store(dcnt - 1, d);
+        dpend = dcnt < DRAIN;
+        if (dpend) drain_read_async(dcnt++, d);
+        load_frags(cur ^ 1, 0, a0, w0);
+        mfmas(a1, w1);
+        interleave();
+        if (tile_end) {  // tile (s / nk) done (nk >= 10: the previous stash is fully drained)
+            int tm0, tn0;
+            tile_origin(s / nk, tm0, tn0);
+            bias_load(tn0);  // this step issued no DMA: the compiler's vmcnt(0) waits for the bias only
+            stash_write(tn0);
+            dm0 = tm0; dn0 = tn0; dcnt = 0;
+            zero();
+            if (s + 2 < S) stage(cur, s + 2);
+        }
+    }
+    {   // last step
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        load_frags((S - 1) & 1, 1, a1, w1);
+        mfmas(a0, w0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        mfmas(a1, w1);
+        __builtin_amdgcn_sched_barrier(0);
+        if (dpend) drain_store(dcnt - 1, d);
+        int m0, n0;
+        tile_origin(my_tiles - 1, m0, n0);
+        bias_load(n0);
+        stash_write(n0);
+        dm0 = m0; dn0 = n0;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    uint4 dl[DRAIN];
+#pragma unroll
+    for (int i = 0; i < DRAIN; ++i) drain_read_async(i, dl[i]);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+    for (int i = 0; i < DRAIN; ++i) drain_store(i, dl[i]);
+}
+
 static int g_num_cus = 0;
 static int num_cus() {
     if (!g_num_cus) {
@@ -809,6 +1090,17 @@ static void launch_persist(hipStream_t s, int epi, const GemmArgs& a) {
         case EPI_F32: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
         case EPI_F32GELU: gemm_persist_kernel<T, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
     }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+static int launch_defer(hipStream_t s, int epi, const GemmArgs& a) {
+    if (a.N % BN || a.K < 640 || !a.bias || (epi != EPI_STORE && epi != EPI_GELU)) return -1;
+    const int V = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
+    const int grid = std::min(V, num_cus());
+    dim3 block(64 * WM * WN);
+    if (epi == EPI_STORE) gemm_defer_kernel<T, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a);
+    else gemm_defer_kernel<T, BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a);
+    return 0;
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -911,6 +1203,14 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 256) return -1;
             launch_pipe<T, 224, 256, 2, 4, 2>(s, epi, a);
             return 0;
+        case 28:  // 8 with non-temporal output stores
+            if (a.N % 256) return -1;
+            launch_pipe<T, 256, 256, 2, 4, 2, true>(s, epi, a);
+            return 0;
+        case 29:  // 21 with non-temporal output stores
+            if (a.N % 256) return -1;
+            launch_pipe<T, 160, 256, 2, 4, 2, true>(s, epi, a);
+            return 0;
         // ---- persistent ring variants ----
         case 24:
             if (a.N % 256) return -1;
@@ -928,6 +1228,25 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 256) return -1;
             launch_persist<T, 128, 256, 2, 4>(s, epi, a);
             return 0;
+        // ---- persistent, deferred (LDS-stashed) epilogue; 16-bit outputs only ----
+        case 30: return launch_defer<T, 128, 256, 2, 4>(s, epi, a);
+        case 31: return launch_defer<T, 128, 256, 4, 2>(s, epi, a);
+        case 34: {  // 30 with non-temporal output stores
+            if (a.N % 256 || a.K < 640 || !a.bias || (epi != EPI_STORE && epi != EPI_GELU)) return -1;
+            const int V = grid_for((a.M + 127) / 128, a.N / 256, a.xcd_n);
+            const int grid = std::min(V, num_cus());
+            if (epi == EPI_STORE) gemm_defer_kernel<T, 128, 256, 2, 4, EPI_STORE, 0, true><<<grid, 512, 0, s>>>(a);
+            else gemm_defer_kernel<T, 128, 256, 2, 4, EPI_GELU, 0, true><<<grid, 512, 0, s>>>(a);
+            return 0;
+        }
+        case 32: case 33: {  // ablations of 30 (timing only): no stores / no stash writes + stores
+            if (a.N % 256 || a.K < 640 || !a.bias) return -1;
+            const int V = grid_for((a.M + 127) / 128, a.N / 256, a.xcd_n);
+            const int grid = std::min(V, num_cus());
+            if (variant == 32) gemm_defer_kernel<T, 128, 256, 2, 4, EPI_STORE, 1><<<grid, 512, 0, s>>>(a);
+            else gemm_defer_kernel<T, 128, 256, 2, 4, EPI_STORE, 3><<<grid, 512, 0, s>>>(a);
+            return 0;
+        }
         case 16: case 17: case 18: case 19: case 20: {  // ablations (timing only)
             if (a.N % 256 || a.K % 32) return -1;
             const int nwg = (a.N / PP_BN) * ((a.M + PP_BM - 1) / PP_BM);

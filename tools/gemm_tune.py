@@ -24,6 +24,7 @@ def main():
     p.add_argument("--iters", type=int, default=20)
     p.add_argument("--dtype", type=int, default=2)
     p.add_argument("--variants", default="1,2,3,4")
+    p.add_argument("--epi", type=int, default=-1, help="force an epilogue (6 = discard ablation)")
     a = p.parse_args()
     torch.cuda.init()
     cfg = get_config(a.model)
@@ -33,6 +34,7 @@ def main():
               ("out", M, D, D, 2), ("fc", M, 4 * D, D, 1), ("proj", M, D, 4 * D, 2)]
     L = _lib.lib()
     for name, m, n, k, epi in shapes:
+        epi = epi if a.epi < 0 else a.epi
         for v in map(int, a.variants.split(",")):
             ms = ctypes.c_float()
             rc = L.clipvit_gemm_bench(a.dtype, m, n, k, epi, v, a.iters, ctypes.byref(ms))
