@@ -13,7 +13,7 @@ from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libclipvit_hip.so"
 
-F32, BF16, F16 = 0, 1, 2
+F32, BF16, F16, MXFP8 = 0, 1, 2, 3
 OK, E_INVALID, E_HIP, E_STATE, E_NOMEM = 0, -1, -2, -3, -4
 
 # Every symbol include/clipvit.h declares (checked by tests/test_abi.py).
@@ -21,7 +21,8 @@ EXPORTS = (
     "clipvit_create", "clipvit_load_weights", "clipvit_load_lora", "clipvit_set_text_features",
     "clipvit_encode_image", "clipvit_classify", "clipvit_text_shape", "clipvit_destroy",
     "clipvit_last_error", "clipvit_abi_version", "clipvit_gemm_test", "clipvit_attention_test",
-    "clipvit_profile_forward", "clipvit_gemm_bench",
+    "clipvit_profile_forward", "clipvit_gemm_bench", "clipvit_quant_mx8_test",
+    "clipvit_gemm_mx8_test",
 )
 
 
@@ -77,6 +78,8 @@ def lib() -> ctypes.CDLL:
             "clipvit_abi_version": (i, []),
             "clipvit_gemm_test": (i, [vp, i, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_attention_test": (i, [vp, i, vp, vp, i, i, i]),
+            "clipvit_quant_mx8_test": (i, [vp, i, vp, i, i, vp, vp]),
+            "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),
             "clipvit_gemm_bench": (i, [i, i, i, i, i, i, i, p_f]),
         }

@@ -69,6 +69,7 @@ struct Lane {
     void* qkv = nullptr; // [cap*N, 3D]
     void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the im2col buffer
     float* f = nullptr;  // [cap, E] projected features
+    unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
 };
@@ -131,6 +132,16 @@ struct clipvit_handle {
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
     int xcd[5] = {2, 2, 2, 2, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
+    // MX-fp8 mode (compute_dtype CLIPVIT_MXFP8): the four Linears of every block run as
+    // MX-fp8 GEMMs (packed weight = N*Kp e4m3 bytes followed by N*Kp/32 E8M0 scales);
+    // patch embedding, attention and everything else stay bf16 / fp32.
+    bool mx8 = false;
+    int var8[4] = {1, 2, 1, 2};  // MX-fp8 GEMM tile per role (qkv, out, fc, proj); CLIPVIT_MX8_VARIANTS
+    // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
+    // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
+    // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
+    uint64_t mx8_skip = 0;
+    bool q8_layer(int i) const { return mx8 && !((mx8_skip >> i) & 1); }
 };
 
 static std::string L(int i, const char* leaf) {
@@ -172,6 +183,7 @@ static int free_ws(Workspace* w) {
         hipFree(l.qkv);
         hipFree(l.u);
         hipFree(l.f);
+        hipFree(l.q8);
         if (l.done) hipEventDestroy(l.done);
         if (l.stream) hipStreamDestroy(l.stream);
     }
@@ -197,6 +209,7 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess) e = hipMalloc(&l.qkv, rows * 3 * h->D * 2);
         if (e == hipSuccess) e = hipMalloc(&l.u, ubytes);
         if (e == hipSuccess) e = hipMalloc((void**)&l.f, (size_t)l.cap * h->E * sizeof(float));
+        if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
     }
@@ -258,10 +271,90 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     return 0;
 }
 
+// MX-fp8 GEMM: A = (A8, A8 + M*K scales), W = packed (N*K e4m3 bytes, then scales).
+static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char* A8,
+                 const void* Wq, const float* bias, void* C, int M, int N, int K, int ldc,
+                 int role) {
+    GemmArgs a{};
+    a.A = A8; a.sA = A8 + (size_t)M * K;
+    a.W = Wq; a.sW = (const unsigned char*)Wq + (size_t)N * K;
+    a.bias = bias; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = ldc;
+    if (epi == EPI_GELU_Q8) a.sC = (unsigned char*)C + (size_t)M * N;
+    a.xcd_n = h->xcd[role];
+    if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, h->var8[role]) != 0 &&
+        launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, 0) != 0) {
+        g_err = "gemm8: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
+                " K=" + std::to_string(K);
+        return CLIPVIT_E_INVALID;
+    }
+    return 0;
+}
+
+// MX-fp8 encoder forward (same sequence as forward()). Blocks listed in
+// mx8_skip run the 16-bit path; every LayerNorm writes the format its consumer block uses.
+static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
+                       Lane* w, float* f_out, Prof* prof) {
+    const int D = h->D, N = h->N, M = B * N;
+    unsigned char* q8 = w->q8;
+    unsigned char* q8s = q8 + (size_t)M * D;
+    unsigned char* u8 = (unsigned char*)w->u;
+    int rc;
+    auto ln = [&](const float* g, const float* b, bool q) {
+        if (q) launch_layernorm_q8(s, w->x, q8, q8s, g, b, M, D);
+        else launch_layernorm(s, h->dt, w->x, w->h, g, b, M, D);
+    };
+    if (prof) prof->mark(s, F_EMBED);
+    launch_im2col(s, in_dtype, h->dt, pix, w->u, B, h->cfg.image_size, h->cfg.patch_size, h->Kp);
+    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, R_PATCH);
+    if (rc) return rc;
+    const LayerW& l0 = h->layers[0];
+    if (h->q8_layer(0))
+        launch_embed_ln_q8(s, w->x, q8, q8s, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
+                           l0.ln1b, B, N, D);
+    else
+        launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
+                        l0.ln1b, B, N, D);
+    if (prof) prof->mark(s, F_EMBED);
+    for (int i = 0; i < h->cfg.layers; ++i) {
+        const LayerW& ly = h->layers[i];
+        const bool q = h->q8_layer(i);
+        rc = q ? gemm8(s, h, EPI_STORE, q8, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)
+               : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV);
+        if (rc) return rc;
+        if (prof) prof->mark(s, F_QKV);
+        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
+        if (prof) prof->mark(s, F_ATTN);
+        rc = q ? gemm8(s, h, EPI_RESID, q8, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT)
+               : gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT);
+        if (rc) return rc;
+        if (prof) prof->mark(s, F_OUT);
+        ln(ly.ln2g, ly.ln2b, q);
+        if (prof) prof->mark(s, F_LN);
+        rc = q ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
+               : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC);
+        if (rc) return rc;
+        if (prof) prof->mark(s, F_FC);
+        rc = q ? gemm8(s, h, EPI_RESID, u8, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)
+               : gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ);
+        if (rc) return rc;
+        if (prof) prof->mark(s, F_PROJ);
+        if (i + 1 < h->cfg.layers) {
+            ln(h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, h->q8_layer(i + 1));
+            if (prof) prof->mark(s, F_LN);
+        }
+    }
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    if (prof) prof->mark(s, F_HEAD);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Encoder forward for B images on stream s with lane buffers w; writes the projected
 // (un-normalised) features to f_out.
 static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
                    Lane* w, float* f_out, Prof* prof) {
+    if (h->mx8) return forward_mx8(h, s, pix, in_dtype, B, w, f_out, prof);
     const int D = h->D, N = h->N, M = B * N;
     int rc;
     if (prof) prof->mark(s, F_EMBED);
@@ -357,7 +450,17 @@ static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name
     int K = 1;
     for (size_t i = 1; i < sh.size(); ++i) K *= (int)sh[i];
     const int Kp = (K + 63) / 64 * 64;
-    launch_pack_weight(s, h->dt, src ? src : h->master[name], dst, N, K, Kp);
+    const float* w = src ? src : h->master[name];
+    int layer = -1;
+    const std::string pre = "visual.transformer.resblocks.";
+    if (name.compare(0, pre.size(), pre) == 0) layer = atoi(name.c_str() + pre.size());
+    if (layer >= 0 && h->q8_layer(layer)) {
+        if (K % 128) FAIL(CLIPVIT_E_INVALID, "MX-fp8 Linear needs in_features % 128 == 0: " + name);
+        unsigned char* q = (unsigned char*)dst;
+        launch_pack_weight_mx8(s, w, q, q + (size_t)N * K, N, K, K);
+        return 0;
+    }
+    launch_pack_weight(s, h->dt, w, dst, N, K, Kp);
     return 0;
 }
 
@@ -376,8 +479,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         FAIL(CLIPVIT_E_INVALID, "width must be a multiple of 256 in [512, 1280]");
     if (c.heads * 64 != c.width) FAIL(CLIPVIT_E_INVALID, "heads * 64 must equal width");
     if (c.embed_dim % 64 || c.embed_dim <= 0) FAIL(CLIPVIT_E_INVALID, "embed_dim % 64 != 0");
-    if (c.compute_dtype != CLIPVIT_BF16 && c.compute_dtype != CLIPVIT_F16)
-        FAIL(CLIPVIT_E_INVALID, "compute_dtype must be BF16 or F16");
+    if (c.compute_dtype != CLIPVIT_BF16 && c.compute_dtype != CLIPVIT_F16 && c.compute_dtype != CLIPVIT_MXFP8)
+        FAIL(CLIPVIT_E_INVALID, "compute_dtype must be BF16, F16 or MXFP8");
     if (c.layers <= 0 || c.max_batch <= 0) FAIL(CLIPVIT_E_INVALID, "layers/max_batch must be > 0");
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
@@ -393,7 +496,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->E = c.embed_dim;
     h->K3 = 3 * c.patch_size * c.patch_size;
     h->Kp = (h->K3 + 63) / 64 * 64;
-    h->dt = c.compute_dtype;
+    h->mx8 = c.compute_dtype == CLIPVIT_MXFP8;
+    h->dt = h->mx8 ? CLIPVIT_BF16 : c.compute_dtype;  // 16-bit type of everything not MX-fp8
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;
@@ -402,6 +506,28 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         int k = 0;
         for (const char* p = v; *p && k < 5; ++k) {
             h->xcd[k] = atoi(p);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+    }
+    if (h->mx8) {
+        const int L = c.layers;
+        for (int b : {0, 1, L - 2, L - 1})
+            if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
+    }
+    if (const char* v = getenv("CLIPVIT_MX8_SKIP")) {  // e.g. "0,11": blocks kept in bf16
+        h->mx8_skip = 0;
+        for (const char* p = v; *p;) {
+            const int b = atoi(p);
+            if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+    }
+    if (const char* v = getenv("CLIPVIT_MX8_VARIANTS")) {
+        int k = 0;
+        for (const char* p = v; *p && k < 4; ++k) {
+            h->var8[k] = atoi(p);
             while (*p && *p != ',') ++p;
             if (*p == ',') ++p;
         }
@@ -743,18 +869,63 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     return 0;
 }
 
+int clipvit_quant_mx8_test(void* stream, int in_dtype, const void* src_dev, int rows, int K,
+                           unsigned char* q_dev, unsigned char* sq_dev) {
+    g_err.clear();
+    if (!src_dev || !q_dev || !sq_dev || rows <= 0 || K <= 0 || K % 32)
+        FAIL(CLIPVIT_E_INVALID, "bad argument");
+    if (in_dtype < 0 || in_dtype > 2) FAIL(CLIPVIT_E_INVALID, "in_dtype");
+    launch_quant_mx8((hipStream_t)stream, in_dtype, src_dev, q_dev, sq_dev, rows, K);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsigned char* sA_dev,
+                          const float* W_dev, const float* bias_dev, void* C_dev,
+                          unsigned char* sC_dev, int M, int N, int K, int epi, int variant) {
+    g_err.clear();
+    if (!A8_dev || !sA_dev || !W_dev || !C_dev || M <= 0) FAIL(CLIPVIT_E_INVALID, "null argument");
+    if (K % 128 || N % 128) FAIL(CLIPVIT_E_INVALID, "K and N must be multiples of 128");
+    if ((epi == 3 || epi == 4) && !sC_dev) FAIL(CLIPVIT_E_INVALID, "sC required for MX-fp8 output");
+    if (epi < 0 || epi > 5) FAIL(CLIPVIT_E_INVALID, "epi");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned char* Wq = nullptr;
+    HIPCHK(hipMallocAsync((void**)&Wq, (size_t)N * K + (size_t)N * K / 32, s));
+    launch_pack_weight_mx8(s, W_dev, Wq, Wq + (size_t)N * K, N, K, K);
+    GemmArgs a{};
+    a.A = A8_dev; a.sA = sA_dev; a.W = Wq; a.sW = Wq + (size_t)N * K;
+    a.bias = bias_dev; a.C = C_dev; a.sC = sC_dev;
+    a.M = M; a.N = N; a.K = K; a.ldc = N;
+    a.xcd_n = variant / 100;
+    static const int emap[6] = {EPI_F32, EPI_F32GELU, EPI_RESID, EPI_Q8, EPI_GELU_Q8, EPI_STORE};
+    const int rc = launch_gemm_mx8(s, CLIPVIT_BF16, emap[epi], a, variant % 100);
+    HIPCHK(hipFreeAsync(Wq, s));
+    if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported MX-fp8 gemm shape/variant");
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int iters,
                        float* avg_ms) {
     g_err.clear();
     if (!avg_ms || iters <= 0 || K % 64 || N % 64 || M <= 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
+    // dtype CLIPVIT_MXFP8: the MX-fp8 GEMM on random e4m3 operands (unit scales); epi 1
+    // (QuickGELU) runs as the production EPI_GELU_Q8, 3 (patch) is not an MX-fp8 role
+    const bool mx = dtype == CLIPVIT_MXFP8;
+    if (mx && (K % 128 || epi == EPI_PATCH)) FAIL(CLIPVIT_E_INVALID, "unsupported MX-fp8 bench shape");
     void *A = nullptr, *W = nullptr, *Cb = nullptr;
     float* bias = nullptr;
     HIPCHK(hipMalloc(&A, (size_t)M * K * 2));
     HIPCHK(hipMalloc(&W, (size_t)N * K * 2));
     HIPCHK(hipMalloc(&Cb, (size_t)M * N * 4));
     HIPCHK(hipMalloc(&bias, (size_t)N * 4));
-    launch_fill_random16(nullptr, dtype, A, (size_t)M * K, 1u);
-    launch_fill_random16(nullptr, dtype, W, (size_t)N * K, 2u);
+    if (mx) {
+        launch_fill_random_mx8(nullptr, (unsigned char*)A, (unsigned char*)A + (size_t)M * K, (size_t)M * K, 1u);
+        launch_fill_random_mx8(nullptr, (unsigned char*)W, (unsigned char*)W + (size_t)N * K, (size_t)N * K, 2u);
+    } else {
+        launch_fill_random16(nullptr, dtype, A, (size_t)M * K, 1u);
+        launch_fill_random16(nullptr, dtype, W, (size_t)N * K, 2u);
+    }
     HIPCHK(hipMemset(bias, 0, (size_t)N * 4));
     HIPCHK(hipMemset(Cb, 0, (size_t)M * N * 4));
     GemmArgs a{};
@@ -763,13 +934,22 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.patch_g2 = 49; a.patch_ntok = 50;
     a.xcd_n = variant / 100;
     variant %= 100;
-    const int e = epi;  // raw Epi enum
-    int rc = launch_gemm(nullptr, dtype, e, a, variant);
+    int e = epi;  // raw Epi enum
+    if (mx) {
+        a.sA = (const unsigned char*)A + (size_t)M * K;
+        a.sW = (const unsigned char*)W + (size_t)N * K;
+        a.sC = (unsigned char*)Cb + (size_t)M * N;
+        if (e == EPI_GELU) e = EPI_GELU_Q8;
+    }
+    auto launch = [&]() {
+        return mx ? launch_gemm_mx8(nullptr, CLIPVIT_BF16, e, a, variant) : launch_gemm(nullptr, dtype, e, a, variant);
+    };
+    int rc = launch();
     hipEvent_t t0, t1;
     hipEventCreate(&t0);
     hipEventCreate(&t1);
     hipEventRecord(t0, nullptr);
-    for (int i = 0; i < iters && !rc; ++i) rc = launch_gemm(nullptr, dtype, e, a, variant);
+    for (int i = 0; i < iters && !rc; ++i) rc = launch();
     hipEventRecord(t1, nullptr);
     hipEventSynchronize(t1);
     float ms = 0.f;

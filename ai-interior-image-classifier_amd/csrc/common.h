@@ -78,6 +78,30 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
                                      0);
 }
 
+// ---- MX-fp8: OCP e4m3 elements, one E8M0 (power-of-two) scale per 32 consecutive K ----
+// Block rule (shared by every producer and by the tests' host reference): e = the smallest
+// integer with amax * 2^-e <= 448 (e4m3's largest finite), clamped to [-127, 126]; scale byte
+// = e + 127; element = RNE-e4m3(x * 2^-e). amax == 0 gives e = -127 and zero elements.
+__device__ __forceinline__ int mx_exp(float amax) {
+    if (!(amax > 0.f)) return -127;
+    int ex;
+    const float m = frexpf(amax * (1.0f / 448.0f), &ex);  // amax/448 = m 2^ex, m in [0.5, 1)
+    int e = m == 0.5f ? ex - 1 : ex;
+    return e < -127 ? -127 : (e > 126 ? 126 : e);
+}
+__device__ __forceinline__ float mx_inv(int e) { return __int_as_float((127 - e) << 23); }  // 2^-e
+// four floats (already scaled) -> four e4m3 bytes, first value in the low byte
+__device__ __forceinline__ unsigned pk4_e4m3(float a, float b, float c, float d) {
+    unsigned r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+}
+
+// s_waitcnt vmcnt(N) as inline asm (hand-counted waits of the glds pipelines)
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // GEMM epilogues.
 enum Epi {
     EPI_STORE = 0,   // C (T)   = acc + bias
@@ -87,6 +111,8 @@ enum Epi {
     EPI_F32 = 4,     // C (f32) = acc + bias                         (tests)
     EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
     EPI_DISCARD = 6, // no stores (epilogue-cost ablation; timing only, pipelined kernel)
+    EPI_GELU_Q8 = 7, // C (MX-fp8) = quickgelu(acc + bias), block scales to sC  (MX-fp8 GEMM)
+    EPI_Q8 = 8,      // C (MX-fp8) = acc + bias, block scales to sC             (tests)
 };
 
 struct GemmArgs {
@@ -97,6 +123,10 @@ struct GemmArgs {
     int M, N, K, ldc;
     int patch_g2, patch_ntok;  // EPI_PATCH row remap: m -> (m / g2) * ntok + 1 + m % g2
     int xcd_n;  // tile->XCD partition: 2 = 4 M-bands x 2 N-halves per XCD group (else 1-D)
+    // MX-fp8 GEMM only: E8M0 block scales [rows][K/32] of A and W, [M][N/32] of a Q8 output
+    const unsigned char* sA;
+    const unsigned char* sW;
+    unsigned char* sC;
 };
 
 // Map a launch-order block id to its (m-tile, n-tile). Blocks b, b+8, ... are observed to
@@ -139,6 +169,19 @@ __host__ __device__ inline int grid_for(int nM, int nN, int xn) {
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
+
+// MX-fp8 path (mx8.hip). out16: 16-bit output type of EPI_STORE (1 bf16, 2 fp16).
+int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant);
+void launch_quant_mx8(hipStream_t s, int in_dtype, const void* src, unsigned char* q,
+                      unsigned char* sq, int rows, int K);
+void launch_fill_random_mx8(hipStream_t s, unsigned char* q, unsigned char* sq, size_t n, unsigned seed);
+void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, unsigned char* sq,
+                            int N, int K, int Kp);
+void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
+                         const float* g, const float* b, int rows, int D);
+void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,
+                        const float* cls, const float* pos, const float* g_pre,
+                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D);
 
 void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n);
 

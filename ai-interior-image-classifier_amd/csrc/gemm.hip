@@ -174,11 +174,6 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_nt_kernel(GemmArgs a) {
 // __syncthreads(), which would drain vmcnt to 0); fragments for the next 32-deep k-substep
 // are read from LDS while the current substep's MFMAs run, and the barrier that hands over
 // tile kt+1 sits between the last ds_read of tile kt and its last MFMAs.
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // Wait until the awaited tile's loads have landed, given r = number of tiles (LPT loads each)
 // issued after it that may stay in flight (0 <= r <= NS - 2).
 template <int LPT, int NS>

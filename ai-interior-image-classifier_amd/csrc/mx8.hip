@@ -1,0 +1,420 @@
+// MX-fp8 path of the encoder's dense contractions (BASELINE.json config 5: fp8 weights, 16-bit
+// activations between kernels, fp32 residual / LayerNorm / softmax).
+//
+// Format (OCP MX): e4m3 elements, one E8M0 power-of-two scale per 32 consecutive K-elements of
+// a row. Weights are quantized once at load time (launch_pack_weight_mx8, same 64-row
+// permutation as the 16-bit packer); GEMM A-operands are quantized by their producers —
+// LayerNorm (ln_1 / ln_2 -> qkv / c_fc), the c_fc epilogue (QuickGELU -> c_proj) and
+// launch_quant_mx8 (attention output -> out_proj). The GEMM runs on
+// v_mfma_scale_f32_16x16x128_f8f6f4 (2x the bf16 MFMA rate, block scales applied in hardware).
+//
+// GEMM kernel = gemm_pipe_kernel's structure (glds 128-B rows, 2-stage LDS ring, swapped
+// operands so a lane owns 16 contiguous output features) at BK = 128 fp8 per k-step:
+//  * operand lane map (measured on MI355X, tools/probes/mx_probe.hip): lane l, g = l >> 4,
+//    holds row l & 15 at k = 16 g + j (bytes j < 16) and k = 64 + 16 g + j - 16 (bytes
+//    j >= 16), i.e. 16-B chunks g and g + 4 of the 128-B row; the E8M0 scale operand of lane
+//    r + 16 b applies to row r, k-block b (= k / 32) -> a lane passes the scale of block g;
+//  * LDS rows are 128 B; 16-B chunk c of row r lives at c ^ (r & 7): chunks g and g + 4 are
+//    the 16-bit kernel's two k-substeps (c = 4 s + g), conflict-free for ds_read_b128;
+//  * per k-step each stage also receives the 4 scale bytes (one dword) of every A and W row
+//    by 4-byte glds; a lane reads its byte with ds_read_u8.
+#include <algorithm>
+#include <type_traits>
+#include "common.h"
+
+namespace clipvit {
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int mx_sw(int r) { return r & 7; }
+
+// ---------------------------------------------------------------------------------------
+// 16-bit (or fp32) [rows][K] -> MX-fp8; one thread per 32-element block.
+template <int IN>
+__global__ void quant_mx8_kernel(const void* __restrict__ src, unsigned char* __restrict__ q,
+                                 unsigned char* __restrict__ sq, long nblk) {
+    const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    float v[32];
+    if constexpr (IN == 0) {
+        const float4* p = (const float4*)src + b * 8;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 t = p[i];
+            v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+        }
+    } else {
+        const uint4* p = (const uint4*)src + b * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 t = p[i];
+            const unsigned w[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const u16 lo = (u16)(w[j] & 0xffff), hi = (u16)(w[j] >> 16);
+                v[8 * i + 2 * j] = IN == 1 ? BF16::to_f32(lo) : F16::to_f32(lo);
+                v[8 * i + 2 * j + 1] = IN == 1 ? BF16::to_f32(hi) : F16::to_f32(hi);
+            }
+        }
+    }
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) a = fmaxf(a, fabsf(v[i]));
+    const int e = mx_exp(a);
+    const float inv = mx_inv(e);
+    unsigned o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = pk4_e4m3(v[4 * i] * inv, v[4 * i + 1] * inv, v[4 * i + 2] * inv, v[4 * i + 3] * inv);
+    uint4* d = (uint4*)q + b * 2;
+    d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    sq[b] = (unsigned char)(e + 127);
+}
+
+void launch_quant_mx8(hipStream_t s, int in_dtype, const void* src, unsigned char* q,
+                      unsigned char* sq, int rows, int K) {
+    const long nblk = (long)rows * (K / 32);
+    const unsigned g = (unsigned)((nblk + 255) / 256);
+    if (in_dtype == 0) quant_mx8_kernel<0><<<g, 256, 0, s>>>(src, q, sq, nblk);
+    else if (in_dtype == 2) quant_mx8_kernel<2><<<g, 256, 0, s>>>(src, q, sq, nblk);
+    else quant_mx8_kernel<1><<<g, 256, 0, s>>>(src, q, sq, nblk);
+}
+
+// Benchmark operands: uniform [-1, 1) values as e4m3 with unit block scales.
+__global__ void fill_random_mx8_kernel(unsigned char* q, unsigned char* sq, size_t n, unsigned seed) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n / 4) return;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        unsigned x = (unsigned)(4 * i + j) * 2654435761u ^ (seed * 0x9E3779B9u);
+        x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+        v[j] = (float)(x >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    }
+    ((unsigned*)q)[i] = pk4_e4m3(v[0], v[1], v[2], v[3]);
+    if ((4 * i) % 32 == 0) sq[4 * i / 32] = 127;
+}
+
+void launch_fill_random_mx8(hipStream_t s, unsigned char* q, unsigned char* sq, size_t n, unsigned seed) {
+    fill_random_mx8_kernel<<<(unsigned)((n / 4 + 255) / 256), 256, 0, s>>>(q, sq, n, seed);
+}
+
+// fp32 [N][K] Linear weight -> MX-fp8 [N][Kp] + scales [N][Kp/32], rows permuted inside each
+// 64-row group exactly as pack_weight_kernel (norm.hip); columns >= K are zero.
+__global__ void pack_weight_mx8_kernel(const float* __restrict__ src, unsigned char* __restrict__ q,
+                                       unsigned char* __restrict__ sq, int N, int K, int Kp) {
+    const long b = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nb = Kp / 32;
+    if (b >= (long)N * nb) return;
+    const int p = (int)(b / nb), kb = (int)(b % nb);
+    const int grp = p & ~63, pi = p & 63, f = pi >> 4, i = pi & 15;
+    const int n = grp + 16 * (i >> 2) + 4 * f + (i & 3);
+    float v[32];
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const int k = kb * 32 + j;
+        v[j] = k < K ? src[(size_t)n * K + k] : 0.f;
+        a = fmaxf(a, fabsf(v[j]));
+    }
+    const int e = mx_exp(a);
+    const float inv = mx_inv(e);
+    unsigned o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = pk4_e4m3(v[4 * j] * inv, v[4 * j + 1] * inv, v[4 * j + 2] * inv, v[4 * j + 3] * inv);
+    uint4* d = (uint4*)(q + (size_t)p * Kp + kb * 32);
+    d[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    d[1] = make_uint4(o[4], o[5], o[6], o[7]);
+    sq[(size_t)p * nb + kb] = (unsigned char)(e + 127);
+}
+
+void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, unsigned char* sq,
+                            int N, int K, int Kp) {
+    const long nblk = (long)N * (Kp / 32);
+    pack_weight_mx8_kernel<<<(unsigned)((nblk + 255) / 256), 256, 0, s>>>(src, q, sq, N, K, Kp);
+}
+
+// ---------------------------------------------------------------------------------------
+// C[M, N] = dequant(A8)[M, K] @ dequant(W8)[N, K]^T (+ bias), fused epilogue.
+template <typename TO, int BM, int BN, int WM, int WN, int EPI>
+__global__ __launch_bounds__(64 * WM* WN) void gemm_mx8_kernel(GemmArgs a) {
+    constexpr int NT = 64 * WM * WN;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int FM = TM / 16, FN = TN / 16;
+    static_assert(TN % 64 == 0 && TM % 16 == 0, "wave tile");
+    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
+    constexpr int LA = (A_BYTES + NT * 16 - 1) / (NT * 16), LW = (W_BYTES + NT * 16 - 1) / (NT * 16);
+    static_assert(A_BYTES % 1024 == 0 && W_BYTES % 1024 == 0, "whole-wave staging pieces");
+    constexpr int SC_ROWS = BM + BN;                      // one scale dword per row per k-step
+    // every wave issues one 4-byte scale glds per k-step (branch-free); waves past the last
+    // scale row fill a pad area
+    constexpr int STAGE = A_BYTES + W_BYTES + (NT > SC_ROWS ? NT : SC_ROWS) * 4;
+    static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "whole staging rounds");
+    // one LDS object per ring stage: with the stage index a compile-time constant at every
+    // use, alias analysis separates the stage being refilled by LDS-DMA from the one being
+    // read, and the compiler does not guard the fragment ds_reads with vmcnt(0)
+    __shared__ __attribute__((aligned(16))) unsigned char smem0[STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char smem1[STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int nN = a.N / BN;
+    int mt, nt;
+    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, nN, a.xcd_n, mt, nt)) return;
+    const int m0 = mt * BM, n0 = nt * BN;
+
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K;          // fp8 row stride in bytes
+    const size_t lds_ = (size_t)(a.K / 32);  // scale row stride
+    const int mlast = a.M - 1;
+    unsigned asrc[LA], wsrc[LW];  // byte offsets (operands < 4 GiB)
+#pragma unroll
+    for (int r = 0; r < LA; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        const int row = p >> 7, c = ((p >> 4) & 7) ^ mx_sw(row & 15);
+        asrc[r] = (unsigned)((size_t)min(m0 + row, mlast) * ldb + c * 16);
+    }
+#pragma unroll
+    for (int r = 0; r < LW; ++r) {
+        const int p = r * NT * 16 + tid * 16;
+        const int row = p >> 7, c = ((p >> 4) & 7) ^ mx_sw(row & 15);
+        wsrc[r] = (unsigned)((size_t)(n0 + row) * ldb + c * 16);
+    }
+    // scale rows: thread t loads row t's dword (A rows first, then W rows; t >= SC_ROWS: pad)
+    static_assert(SC_ROWS <= NT, "one scale dword per thread");
+    const unsigned char* ssrc = tid < BM ? a.sA + (size_t)min(m0 + tid, mlast) * lds_
+                              : tid < SC_ROWS ? a.sW + (size_t)(n0 + tid - BM) * lds_
+                                              : a.sW + (size_t)n0 * lds_;
+
+    auto stage = [&](auto B, int kt) {
+        unsigned char* sA = decltype(B)::value ? smem1 : smem0;
+        unsigned char* sW = sA + A_BYTES;
+        unsigned char* sS = sW + W_BYTES;
+        const unsigned kofs = (unsigned)kt * 128;
+#pragma unroll
+        for (int r = 0; r < LA; ++r) glds16(Ab + (asrc[r] + kofs), sA + r * NT * 16 + wave * 1024);
+#pragma unroll
+        for (int r = 0; r < LW; ++r) glds16(Wb + (wsrc[r] + kofs), sW + r * NT * 16 + wave * 1024);
+        __builtin_amdgcn_global_load_lds((const GLB_AS void*)(ssrc + kt * 4),
+                                         (LDS_AS void*)(sS + wave * 256), 4, 0, 0);
+    };
+
+    const int lrow = lane & 15, lg = lane >> 4;
+    // fragment addresses: rows of a lane's fragments differ by multiples of 16, so the
+    // swizzle depends on lrow only and every fragment is base + compile-time offset
+    const int fsw = mx_sw(lrow);
+    const int c0 = (lg ^ fsw) << 4, c1 = ((lg + 4) ^ fsw) << 4;
+    const int fa = (wm * TM + lrow) * 128;
+    const int fw = A_BYTES + (wn * TN + lrow) * 128;
+    const int fsa = A_BYTES + W_BYTES + (wm * TM + lrow) * 4 + lg;
+    const int fsw_ = A_BYTES + W_BYTES + (BM + wn * TN + lrow) * 4 + lg;
+    auto frag = [&](const unsigned char* p) -> i32x8 {
+        const uint4 lo = *(const uint4*)(p + c0);
+        const uint4 hi = *(const uint4*)(p + c1);
+        return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    };
+    constexpr int FH = FN / 2;  // W fragments per half k-step
+    static_assert(FN % 2 == 0, "two W halves");
+    auto load_a = [&](auto B, i32x8 (&af)[FM], int (&as)[FM]) {
+        const unsigned char* sb = decltype(B)::value ? smem1 : smem0;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            af[fm] = frag(sb + fa + fm * 2048);
+            as[fm] = sb[fsa + fm * 64];
+        }
+    };
+    auto load_w = [&](auto B, int half, i32x8 (&wf)[FH], int (&ws)[FH]) {
+        const unsigned char* sb = decltype(B)::value ? smem1 : smem0;
+#pragma unroll
+        for (int j = 0; j < FH; ++j) {
+            const int fn = half * FH + j;
+            wf[j] = frag(sb + fw + fn * 2048);
+            ws[j] = sb[fsw_ + fn * 64];
+        }
+    };
+
+    f32x4 acc[FN][FM];
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfmas = [&](int half, const i32x8 (&af)[FM], const int (&as)[FM], const i32x8 (&wf)[FH],
+                     const int (&ws)[FH]) {
+#pragma unroll
+        for (int j = 0; j < FH; ++j)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm)
+                acc[half * FH + j][fm] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    wf[j], af[fm], acc[half * FH + j][fm], 0, 0, 0, ws[j], 0, as[fm]);
+    };
+    // interleave n reads (3 instructions per fragment) one-per-MFMA into a block of FH*FM MFMAs
+    auto interleave = [&](auto NRD) {
+        constexpr int nrd = decltype(NRD)::value;
+#pragma unroll
+        for (int i = 0; i < FH * FM; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (i < nrd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        if constexpr (nrd > FH * FM) __builtin_amdgcn_sched_group_barrier(0x100, nrd - FH * FM, 0);
+    };
+
+    // K-step kt (stage kt & 1) runs as two MFMA blocks over the two W halves, exactly like the
+    // 16-bit pipe kernel's two k-substeps: block 0 runs while the second W half is read;
+    // then, after the barrier that hands over stage kt+1 (and frees stage kt for k-step kt+2),
+    // block 1 runs while the next step's A fragments and first W half are read.
+    // Registers: A fragments x2 (current, next), W halves x2, accumulators.
+    const int nk = a.K >> 7;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    stage(P0{}, 0);
+    vm_wait<0>();
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) stage(P1{}, 1);
+    i32x8 a0[FM], a1[FM], wl[FH], wh[FH];
+    int sa0[FM], sa1[FM], swl[FH], swh[FH];
+    load_a(P0{}, a0, sa0);
+    load_w(P0{}, 0, wl, swl);
+
+    // k-step with a successor (kt + 1 < nk)
+    auto kstep = [&](int kt, auto P, i32x8 (&ac)[FM], int (&sac)[FM], i32x8 (&an)[FM], int (&san)[FM]) {
+        constexpr int cur = decltype(P)::value;
+        using PN = std::integral_constant<int, cur ^ 1>;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // A fragments + first W half of stage kt landed
+        load_w(P, 1, wh, swh);
+        mfmas(0, ac, sac, wl, swl);
+        interleave(std::integral_constant<int, 3 * FH>{});
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // stage kt fully read
+        vm_wait<0>();                        // stage kt+1 landed (own loads)
+        __builtin_amdgcn_s_barrier();        // ... everyone's; nobody reads stage kt any more
+        // branch-free: past the end the freed stage is refilled with a real (unused) k-step,
+        // which keeps the loop body one basic block (no MFMA sinking past the barriers)
+        stage(P, min(kt + 2, nk - 1));
+        load_a(PN{}, an, san);
+        load_w(PN{}, 0, wl, swl);
+        mfmas(1, ac, sac, wh, swh);
+        interleave(std::integral_constant<int, 3 * (FM + FH)>{});
+    };
+    auto klast = [&](auto P, i32x8 (&ac)[FM], int (&sac)[FM]) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        load_w(P, 1, wh, swh);
+        mfmas(0, ac, sac, wl, swl);
+        interleave(std::integral_constant<int, 3 * FH>{});
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        mfmas(1, ac, sac, wh, swh);
+    };
+    int kt = 0;
+    for (; kt + 2 < nk; kt += 2) {  // pairs of k-steps that both have a successor
+        kstep(kt, P0{}, a0, sa0, a1, sa1);
+        kstep(kt + 1, P1{}, a1, sa1, a0, sa0);
+    }
+    if (kt + 2 == nk) {
+        kstep(kt, P0{}, a0, sa0, a1, sa1);
+        klast(P1{}, a1, sa1);
+    } else {
+        klast(P0{}, a0, sa0);
+    }
+
+    // ---- epilogue: lane (lrow, g) owns token m, 16 contiguous features n .. n+15 ----
+    const int g = lg;
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = m0 + wm * TM + fm * 16 + lrow;
+#pragma unroll
+        for (int q = 0; q < FN / 4; ++q) {
+            const int n = n0 + wn * TN + q * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
+            if (a.bias) {
+                const float4* b4 = (const float4*)(a.bias + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float4 bb = b4[i];
+                    v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                }
+            }
+            if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_F32GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+            }
+            if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_Q8) {
+                // MX block = 32 features = this lane's 16 + those of lane ^ 16 (same token)
+                float am = 0.f;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) am = fmaxf(am, fabsf(v[i]));
+                am = fmaxf(am, __shfl_xor(am, 16, 64));
+                if (m >= a.M) continue;
+                const int e = mx_exp(am);
+                const float inv = mx_inv(e);
+                *(uint4*)((unsigned char*)a.C + (size_t)m * a.ldc + n) =
+                    make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
+                               pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
+                               pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
+                               pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
+                if ((g & 1) == 0) a.sC[(size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
+                continue;
+            }
+            if (m >= a.M) continue;
+            if constexpr (EPI == EPI_STORE) {
+                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+                dst[0] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                    pack2<TO>(v[6], v[7]));
+                dst[1] = make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]),
+                                    pack2<TO>(v[12], v[13]), pack2<TO>(v[14], v[15]));
+            } else if constexpr (EPI == EPI_RESID) {
+                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    float4 o = dst[i];
+                    o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                    dst[i] = o;
+                }
+            } else {  // EPI_F32 / EPI_F32GELU
+                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+            }
+        }
+    }
+}
+
+template <typename TO, int BM, int BN, int WM, int WN>
+static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
+    if (a.N % BN) return -1;
+    const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
+    dim3 grid(nwg), block(64 * WM * WN);
+    switch (epi) {
+        case EPI_STORE: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU_Q8: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_GELU_Q8><<<grid, block, 0, s>>>(a); break;
+        case EPI_Q8: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_Q8><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
+        case EPI_F32GELU: gemm_mx8_kernel<TO, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+        default: return -1;
+    }
+    return 0;
+}
+
+// variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves)
+template <typename TO>
+static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
+    if (variant == 0) variant = a.N % 256 == 0 ? 1 : 2;
+    switch (variant) {
+        case 1: return launch_mx8_tile<TO, 128, 256, 2, 4>(s, epi, a);
+        case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
+    }
+    return -1;
+}
+
+int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant) {
+    if (a.K % 128 != 0 || a.M <= 0 || !a.sA || !a.sW) return -1;
+    if ((epi == EPI_GELU_Q8 || epi == EPI_Q8) && (!a.sC || a.ldc % 32)) return -1;
+    if (out16 == 2) return launch_mx8_t<F16>(s, epi, a, variant);
+    return launch_mx8_t<BF16>(s, epi, a, variant);
+}
+
+}  // namespace clipvit

@@ -123,9 +123,31 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
     }
 }
 
+// MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
+// block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
+// E8M0 scale (rule: common.h mx_exp).
+template <int V>
+__device__ __forceinline__ void store_row_q8(unsigned char* q, unsigned char* sq,
+                                             const float4 (&v)[V], int lane) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        float a = fmaxf(fmaxf(fabsf(v[i].x), fabsf(v[i].y)), fmaxf(fabsf(v[i].z), fabsf(v[i].w)));
+        a = fmaxf(a, __shfl_xor(a, 1, 64));
+        a = fmaxf(a, __shfl_xor(a, 2, 64));
+        a = fmaxf(a, __shfl_xor(a, 4, 64));
+        const int e = mx_exp(a);
+        const float inv = mx_inv(e);
+        *(unsigned*)(q + c) = pk4_e4m3(v[i].x * inv, v[i].y * inv, v[i].z * inv, v[i].w * inv);
+        if ((lane & 7) == 0) sq[c >> 5] = (unsigned char)(e + 127);
+    }
+}
+
 // x[row] = ln_pre((t == 0 ? class_embedding : patch_row) + pos[t]);  h[row] = ln_1(x[row])
-template <typename T, int V>
-__global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, u16* __restrict__ h,
+// (Q8: h as MX-fp8 q [rows][D] + scales sq [rows][D/32])
+template <typename T, int V, bool Q8 = false>
+__global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, void* __restrict__ h,
+                                                       unsigned char* __restrict__ sq,
                                                        const float* __restrict__ cls,
                                                        const float* __restrict__ pos,
                                                        const float* __restrict__ gp,
@@ -152,12 +174,14 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, u1
 #pragma unroll
     for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
     ln_row<V>(v, g1, b1, lane, (float)D);
-    store_row16<T, V>(h + (size_t)row * D, v, lane);
+    if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v, lane);
+    else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
-template <typename T, int V>
+template <typename T, int V, bool Q8 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x,
-                                                        u16* __restrict__ h,
+                                                        void* __restrict__ h,
+                                                        unsigned char* __restrict__ sq,
                                                         const float* __restrict__ gm,
                                                         const float* __restrict__ bt, int rows) {
     const int lane = threadIdx.x & 63;
@@ -169,7 +193,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
     for (int i = 0; i < V; ++i) v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
     ln_row<V>(v, gm, bt, lane, (float)D);
-    store_row16<T, V>(h + (size_t)row * D, v, lane);
+    if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v, lane);
+    else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
 #define DISPATCH_V(D, ...)                          \
@@ -187,19 +212,33 @@ void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* c
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
-        DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)h, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+        DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N));
     } else {
-        DISPATCH_V(D, embed_ln_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)h, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+        DISPATCH_V(D, embed_ln_kernel<BF16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N));
     }
+}
+
+void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,
+                        const float* cls, const float* pos, const float* g_pre,
+                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D) {
+    const int rows = B * N;
+    dim3 grid((rows + 3) / 4), block(256);
+    DISPATCH_V(D, embed_ln_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+}
+
+void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
+                         const float* g, const float* b, int rows, int D) {
+    dim3 grid((rows + 3) / 4), block(256);
+    DISPATCH_V(D, layernorm_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, g, b, rows));
 }
 
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
                       const float* b, int rows, int D) {
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
-        DISPATCH_V(D, layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)h, g, b, rows));
+        DISPATCH_V(D, layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, h, nullptr, g, b, rows));
     } else {
-        DISPATCH_V(D, layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)h, g, b, rows));
+        DISPATCH_V(D, layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, h, nullptr, g, b, rows));
     }
 }
 

@@ -18,7 +18,7 @@ from .lora import LoraAdapter
 from .weights import as_host_f32, visual_names
 
 _DT = {"bf16": _lib.BF16, "fp16": _lib.F16, "f16": _lib.F16, torch.bfloat16: _lib.BF16,
-       torch.float16: _lib.F16}
+       torch.float16: _lib.F16, "mxfp8": _lib.MXFP8}
 _PIX_DT = {torch.float32: _lib.F32, torch.bfloat16: _lib.BF16, torch.float16: _lib.F16}
 
 
@@ -200,6 +200,48 @@ def gemm_test(A: torch.Tensor, W: torch.Tensor, bias: torch.Tensor | None, epi: 
                                        K, epi, variant))
         torch.cuda.current_stream(A.device).synchronize()
     return C
+
+
+def quant_mx8_test(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """MX-fp8 quantization of a [rows, K] fp32/bf16/fp16 device tensor by the library's
+    kernel: (e4m3 bytes [rows, K] uint8, E8M0 scales [rows, K/32] uint8)."""
+    L = _lib.lib()
+    x = x.contiguous()
+    rows, K = x.shape
+    q = torch.empty((rows, K), dtype=torch.uint8, device=x.device)
+    sq = torch.empty((rows, K // 32), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(L.clipvit_quant_mx8_test(s, _PIX_DT[x.dtype], _vp(x), rows, K, _vp(q), _vp(sq)))
+        torch.cuda.current_stream(x.device).synchronize()
+    return q, sq
+
+
+def gemm_mx8_test(A8: torch.Tensor, sA: torch.Tensor, W: torch.Tensor, bias: torch.Tensor | None,
+                  epi: int = 0, variant: int = 0, C: torch.Tensor | None = None):
+    """MX-fp8 GEMM through the library (clipvit_gemm_mx8_test). epi 0/1/2 -> fp32 C,
+    3/4 -> (C uint8 [M,N], sC uint8 [M,N/32]), 5 -> bf16 C."""
+    L = _lib.lib()
+    M, K = A8.shape
+    N = W.shape[0]
+    dev = A8.device
+    sC = None
+    if C is None:
+        if epi in (0, 1, 2):
+            C = torch.zeros((M, N), dtype=torch.float32, device=dev)
+        elif epi in (3, 4):
+            C = torch.zeros((M, N), dtype=torch.uint8, device=dev)
+        else:
+            C = torch.zeros((M, N), dtype=torch.bfloat16, device=dev)
+    if epi in (3, 4):
+        sC = torch.zeros((M, N // 32), dtype=torch.uint8, device=dev)
+    W32 = W.float().contiguous()
+    with torch.cuda.device(dev):
+        s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _lib.check(L.clipvit_gemm_mx8_test(s, _vp(A8), _vp(sA), _vp(W32), _vp(bias), _vp(C), _vp(sC),
+                                           M, N, K, epi, variant))
+        torch.cuda.current_stream(dev).synchronize()
+    return (C, sC) if epi in (3, 4) else C
 
 
 def attention_test(qkv: torch.Tensor, B: int, N: int, H: int) -> torch.Tensor:

@@ -40,11 +40,13 @@ typedef enum {
     CLIPVIT_F32 = 0,
     CLIPVIT_BF16 = 1,
     CLIPVIT_F16 = 2,
+    CLIPVIT_MXFP8 = 3, /* compute_dtype only: MX-fp8 Linears (e4m3 + E8M0 per 32), bf16 elsewhere */
 } clipvit_dtype;
 
 /* Model geometry. Mirrors OpenAI-CLIP VisionTransformer(input_resolution, patch_size,
  * width, layers, heads, output_dim) as built by clip.load [3p] for the name passed at
- * main.py:152 / main.py:241.  compute_dtype selects the MFMA operand type (BF16 or F16);
+ * main.py:152 / main.py:241.  compute_dtype selects the MFMA operand type (BF16 or F16, or
+ * MXFP8: the 4 Linears of every block in MX-fp8 with bf16 attention / patch embedding);
  * the residual stream, LayerNorm statistics, softmax and the head stay fp32. */
 typedef struct {
     int image_size;     /* 224 (B/32, B/16) or 336 (L/14@336)          */
@@ -53,7 +55,7 @@ typedef struct {
     int layers;         /* 12 / 24                                      */
     int heads;          /* width / 64                                   */
     int embed_dim;      /* 512 / 768   (multiple of 64)                 */
-    int compute_dtype;  /* CLIPVIT_BF16 or CLIPVIT_F16                  */
+    int compute_dtype;  /* CLIPVIT_BF16, CLIPVIT_F16 or CLIPVIT_MXFP8    */
     int max_batch;      /* largest B accepted by encode/classify        */
 } clipvit_config;
 
@@ -156,6 +158,21 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
  * 0 store16, 1 gelu16, 2 resid32, 3 patch32, 4 f32, 5 f32gelu). Default stream. */
 int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int iters,
                        float* avg_ms);
+
+/* MX-fp8 quantization of a row-major [rows, K] buffer (in_dtype F32/BF16/F16, K % 32 == 0):
+ * q [rows, K] OCP e4m3 bytes, sq [rows, K/32] E8M0 block scales (block = 32 consecutive
+ * columns; scale exponent = smallest e with amax * 2^-e <= 448, clamped to [-127, 126]). */
+int clipvit_quant_mx8_test(void* stream, int in_dtype, const void* src_dev, int rows, int K,
+                           unsigned char* q_dev, unsigned char* sq_dev);
+
+/* MX-fp8 GEMM: A = (A8 [M,K] e4m3, sA [M,K/32]); W fp32 [N,K] natural order (quantized and
+ * packed internally by the load-time packer); bias fp32 [N] or NULL. K % 128 == 0,
+ * N % 128 == 0. epi: 0 C fp32 = A W^T + b; 1 QuickGELU of that; 2 C fp32 += A W^T + b;
+ * 3 C = MX-fp8 of (A W^T + b) [M,N] bytes with scales sC [M,N/32]; 4 = 3 after QuickGELU;
+ * 5 C bf16 [M,N]. variant: 0 auto, 1 128x256, 2 128x128; + 100 * XCD partition. */
+int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsigned char* sA_dev,
+                          const float* W_dev, const float* bias_dev, void* C_dev,
+                          unsigned char* sC_dev, int M, int N, int K, int epi, int variant);
 
 /* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
  * out [B*N, H*64] of `dtype`. */
