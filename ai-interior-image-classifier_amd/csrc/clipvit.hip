@@ -848,7 +848,10 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
-    if (variant >= 30 && variant < 40) {  // 16-bit-output kernels: run, then widen to fp32
+    // 16-bit-output kernels (variants 30-39, or epi 10 / 11 = 16-bit STORE / GELU on any
+    // variant): run, then widen to fp32
+    if ((variant >= 30 && variant < 40) || epi >= 10) {
+        if (epi >= 10) epi -= 10;
         if (epi == 2) {
             hipFreeAsync(Wp, s);
             FAIL(CLIPVIT_E_INVALID, "variant has no residual epilogue");

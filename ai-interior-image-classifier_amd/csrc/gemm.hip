@@ -23,6 +23,7 @@
 //    (x * sigmoid(1.702 x), CLIP's activation) or the fp32 residual add;
 //  * bijective XCD-aware block remap: consecutive logical tiles (same A panel) share an XCD L2.
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 
 namespace clipvit {
@@ -187,7 +188,9 @@ __device__ __forceinline__ void wait_tile(int r) {
     vm_wait<0>();
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, bool NTS = false>
+// ABL (timing-only ablation builds, results wrong): bit0 no global->LDS loads, bit1 no LDS
+// fragment reads, bit2 no MFMAs.
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int ABL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
@@ -232,6 +235,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         wsrc[r] = (size_t)(n0 + row) * ldb + c * 16;
     }
     auto stage = [&](int buf, int kt) {
+        if constexpr (ABL & 1) return;
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = (size_t)kt * 128;
@@ -248,6 +252,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
     const int aoff = (wm * TM + lrow) * 128, woff = A_BYTES + (wn * TN + lrow) * 128;
     auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) asm volatile("" : "=v"(af[fm]));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) asm volatile("" : "=v"(wf[fn]));
+            return;
+        }
         const unsigned char* base = smem + buf * STAGE;
         const int c = (((s << 2) | lg) ^ lsw) << 4;
 #pragma unroll
@@ -287,6 +298,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
 
     auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+        if constexpr (ABL & 4) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) asm volatile("" ::"v"(af[fm]));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) asm volatile("" ::"v"(wf[fn]));
+            return;
+        }
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
@@ -320,6 +338,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 
     // ---- epilogue (same contract as gemm_nt_kernel) ----
     const int g = lg;
+    OutStore<SM> out(a.C);
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
         const int m = m0 + wm * TM + fm * 16 + lrow;
@@ -347,18 +366,19 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                 for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
-                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
-                st16<NTS>(dst, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
-                                          pack2<T>(v[6], v[7])));
-                st16<NTS>(dst + 1, make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
-                                              pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
+                const size_t off = ((size_t)m * a.ldc + n) * 2;
+                out.u4(off, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                       pack2<T>(v[6], v[7])));
+                out.u4(off + 16, make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                            pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
             } else if constexpr (EPI == EPI_RESID) {
-                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+                const float4* src = (const float4*)((float*)a.C + (size_t)m * a.ldc + n);
+                const size_t off = ((size_t)m * a.ldc + n) * 4;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    float4 o = dst[i];
+                    float4 o = src[i];
                     o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
-                    st16f<NTS>(dst + i, o);
+                    out.f4(off + 16 * i, o);
                 }
             } else if constexpr (EPI == EPI_DISCARD) {
                 float t = 0.f;
@@ -369,10 +389,10 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                 size_t row = (size_t)m;
                 if constexpr (EPI == EPI_PATCH)
                     row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
-                float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+                const size_t off = (row * a.ldc + n) * 4;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
-                    dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+                    out.f4(off + 16 * i, make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]));
             }
         }
     }
@@ -401,7 +421,7 @@ __device__ __forceinline__ void sbar() {
 }
 
 // ABL (timing-only ablation builds, results wrong): bit0 no global->LDS loads in the loop,
-// bit1 no LDS fragment reads in the loop, bit2 no barriers in the loop.
+// bit1 no LDS fragment reads in the loop, bit2 no barriers in the loop, bit3 no MFMAs.
 template <typename T, int EPI, int ABL = 0>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
@@ -480,10 +500,15 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
         if (!(ABL & 4)) sbar();
         // M0
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (ABL & 8) {
 #pragma unroll
-        for (int fm = 0; fm < 4; ++fm)
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]), "v"(wf[i]));
+        } else {
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+        }
         __builtin_amdgcn_s_setprio(0);
         if (!(ABL & 4)) sbar();
         // R1: fragments for cluster 1 (A rows 64-127), second half-load of t+3, tile t+1 landed
@@ -502,11 +527,16 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmArgs a) {
         if (!(ABL & 4)) sbar();
         // M1
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (ABL & 8) {
 #pragma unroll
-        for (int fm = 0; fm < 4; ++fm)
+            for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(af[i]), "v"(wf[i]));
+        } else {
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn)
-                acc[fn][4 + fm] = T::mfma16(wf[fn], af[fm], acc[fn][4 + fm]);
+            for (int fm = 0; fm < 4; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < 4; ++fn)
+                    acc[fn][4 + fm] = T::mfma16(wf[fn], af[fm], acc[fn][4 + fm]);
+        }
         __builtin_amdgcn_s_setprio(0);
         if (!(ABL & 4)) sbar();
     }
@@ -578,16 +608,16 @@ static void launch_pp(hipStream_t s, int epi, const GemmArgs& a) {
     }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, bool NTS = false>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int SM = 0>
 static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
     dim3 grid(nwg), block(64 * WM * WN);
-    if constexpr (NTS) {  // non-temporal-store builds: production epilogues only
+    if constexpr (SM != 0) {  // non-temporal / write-through store builds: production epilogues only
         switch (epi) {
-            case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE, true><<<grid, block, 0, s>>>(a); break;
-            case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU, true><<<grid, block, 0, s>>>(a); break;
-            case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID, true><<<grid, block, 0, s>>>(a); break;
-            default: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
+            case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE, SM><<<grid, block, 0, s>>>(a); break;
+            case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU, SM><<<grid, block, 0, s>>>(a); break;
+            case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID, SM><<<grid, block, 0, s>>>(a); break;
+            default: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32, SM><<<grid, block, 0, s>>>(a); break;
         }
         return;
     }
@@ -1200,12 +1230,49 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             return 0;
         case 28:  // 8 with non-temporal output stores
             if (a.N % 256) return -1;
-            launch_pipe<T, 256, 256, 2, 4, 2, true>(s, epi, a);
+            launch_pipe<T, 256, 256, 2, 4, 2, 1>(s, epi, a);
             return 0;
         case 29:  // 21 with non-temporal output stores
             if (a.N % 256) return -1;
-            launch_pipe<T, 160, 256, 2, 4, 2, true>(s, epi, a);
+            launch_pipe<T, 160, 256, 2, 4, 2, 1>(s, epi, a);
             return 0;
+        // ---- write-through (sc1) output stores: 50 = 8, 51 = 21, 52 = 13, 53 = 14 ----
+        case 50:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 256, 256, 2, 4, 2, 2>(s, epi, a);
+            return 0;
+        case 51:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 160, 256, 2, 4, 2, 2>(s, epi, a);
+            return 0;
+        case 52:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 128, 128, 4, 2, 2, 2>(s, epi, a);
+            return 0;
+        case 53:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 192, 256, 2, 4, 2, 2>(s, epi, a);
+            return 0;
+        // ---- ablations of 8 (timing only, results wrong): 60 no loads, 61 no LDS reads,
+        //      62 no MFMAs, 63 MFMAs only (+barriers), 64 loads only (+barriers) ----
+        case 60: case 61: case 62: case 63: case 64: {
+            if (a.N % 256) return -1;
+            const int nwg = grid_for((a.M + 255) / 256, a.N / 256, a.xcd_n);
+            const int e = epi == EPI_DISCARD ? EPI_DISCARD : EPI_STORE;
+            auto L = [&](auto abl) {
+                constexpr int AB = decltype(abl)::value;
+                if (e == EPI_DISCARD) gemm_pipe_kernel<T, 256, 256, 2, 4, 2, EPI_DISCARD, 0, AB><<<nwg, 512, 0, s>>>(a);
+                else gemm_pipe_kernel<T, 256, 256, 2, 4, 2, EPI_STORE, 0, AB><<<nwg, 512, 0, s>>>(a);
+            };
+            switch (variant) {
+                case 60: L(std::integral_constant<int, 1>{}); break;
+                case 61: L(std::integral_constant<int, 2>{}); break;
+                case 62: L(std::integral_constant<int, 4>{}); break;
+                case 63: L(std::integral_constant<int, 3>{}); break;
+                case 64: L(std::integral_constant<int, 6>{}); break;
+            }
+            return 0;
+        }
         // ---- persistent ring variants ----
         case 24:
             if (a.N % 256) return -1;
@@ -1242,10 +1309,12 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             else gemm_defer_kernel<T, 128, 256, 2, 4, EPI_STORE, 3><<<grid, 512, 0, s>>>(a);
             return 0;
         }
-        case 16: case 17: case 18: case 19: case 20: {  // ablations (timing only)
+        case 16: case 17: case 18: case 19: case 20: case 65: case 66: {  // ablations (timing only)
             if (a.N % 256 || a.K % 32) return -1;
             const int nwg = (a.N / PP_BN) * ((a.M + PP_BM - 1) / PP_BM);
             const int abl[5] = {1, 2, 4, 3, 7};
+            if (variant == 65) { gemm_pp_kernel<T, EPI_F32, 10><<<nwg, 512, 0, s>>>(a); return 0; }  // loads only
+            if (variant == 66) { gemm_pp_kernel<T, EPI_F32, 3><<<nwg, 512, 0, s>>>(a); return 0; }   // MFMA only
             switch (abl[variant - 16]) {
                 case 1: gemm_pp_kernel<T, EPI_F32, 1><<<nwg, 512, 0, s>>>(a); break;
                 case 2: gemm_pp_kernel<T, EPI_F32, 2><<<nwg, 512, 0, s>>>(a); break;
@@ -1261,6 +1330,8 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
+    if (variant >= 40 && variant < 50) return launch_gemm_ps(s, dtype, epi, a, variant, num_cus());
+    if (variant >= 70 && variant < 80) return launch_gemm_deep(s, dtype, epi, a, variant);
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);
     return launch_t<BF16>(s, epi, a, variant);
 }

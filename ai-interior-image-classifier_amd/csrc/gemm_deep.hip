@@ -1,0 +1,251 @@
+// Deep-ring 256x256 MFMA GEMM (gfx950, wave64): C[M, N] = A[M, K] @ W[N, K]^T (+ bias), with
+// the fused epilogues of gemm.hip (same packed-weight contract: lane owns 16 contiguous outputs).
+//
+// Why (ablations of the 2-stage 256x256 kernel on the QKV shape, profiles/r01_gemm_pmc.md):
+// its global->LDS loads alone take 29 us and its MFMAs alone 27.5 us, but together 41 us
+// (+12.5 us epilogue): the loads do not overlap the MFMAs because the 2-stage ring drains the
+// load queue to zero at every k-step (`vmcnt(0)`) and then refills 64 KB in one burst. LDS-DMA
+// throughput per CU is set by the bytes in flight (~1.1 us issue->landed latency), so here
+//  * K-steps are 32 deep (a stage = A 256 x 32 + W 256 x 32 = 32 KB) and the ring has NS = 3 or
+//    5 stages: stage t + NS - 1 is issued at step t, so NS - 2 stages stay in flight across
+//    every barrier (counted `s_waitcnt vmcnt`, raw `s_barrier`, never a drain in the loop);
+//  * one barrier per step; the next step's fragments are read while this step's 32 MFMAs run,
+//    with the 4 global->LDS copies and 12 fragment reads interleaved one per MFMA;
+//  * the accumulators start at the bias (read before any copy is in flight), so no epilogue
+//    load makes hipcc drain the queue.
+// LDS rows are 64 B; 16-B chunk c of row r lives at chunk c ^ ((r >> 2) & 2), which makes every
+// ds_read_b128 fragment wave-instruction conflict-free (all 16 lanes of each hardware lane
+// group hit distinct 16-B bank slots); glds writes lane-linearly, so the same involution is
+// applied to the per-lane global source address.
+#include <algorithm>
+#include "common.h"
+
+namespace clipvit {
+
+namespace {
+
+template <int N>
+__device__ __forceinline__ void vm_wait_le(int n) {  // s_waitcnt vmcnt(n), n <= 3 N (multiple of N)
+    if (n >= 3 * N) vm_wait<3 * N>();
+    else if (n >= 2 * N) vm_wait<2 * N>();
+    else if (n >= N) vm_wait<N>();
+    else vm_wait<0>();
+}
+
+template <typename T, int NS, int EPI>
+__global__ __launch_bounds__(512) void gemm_deep_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    static_assert(NS == 3 || NS == 5, "ring depth: NS - 1 must be even (loop unrolled by 2)");
+    constexpr int BM = 256, BN = 256;
+    constexpr int FM = 8, FN = 4;         // wave tile 128 x 64; waves 2 (M) x 4 (N)
+    constexpr int STAGE = (BM + BN) * 64;  // 32 KB
+    constexpr int LPS = 4;                 // global->LDS copies per thread per stage
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    int mt, nt;
+    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, a.N / BN, a.xcd_n, mt, nt)) return;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int lrow = lane & 15, lg = lane >> 4;
+
+    // acc[fn][*] of lane (j, g) holds features n0 + 64 wn + 16 g + 4 fn + r (packed-weight order)
+    f32x4 acc[FN][FM];
+    {
+        f32x4 bv[FN];
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) {
+            bv[fn] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI != EPI_PATCH)
+                if (a.bias) bv[fn] = *(const f32x4*)(a.bias + n0 + wn * 64 + 16 * lg + 4 * fn);
+            asm volatile("" ::"v"(bv[fn]));  // wait for the bias here, before any glds is issued
+        }
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = bv[fn];
+    }
+
+    // ---- staging: copy j (0, 1) of a thread moves rows 128 j + 16 wave + lane / 4 of A and W
+    const unsigned char* Ab = (const unsigned char*)a.A;
+    const unsigned char* Wb = (const unsigned char*)a.W;
+    const size_t ldb = (size_t)a.K * 2;
+    size_t asrc[2], wsrc[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int row = j * 128 + wave * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ ((row >> 2) & 2);
+        asrc[j] = (size_t)min(m0 + row, a.M - 1) * ldb + c * 16;
+        wsrc[j] = (size_t)(n0 + row) * ldb + c * 16;
+    }
+    auto stage = [&](int t) {
+        unsigned char* dst = smem + (t % NS) * STAGE + wave * 1024;
+        const size_t kofs = (size_t)t * 64;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            glds16(Ab + asrc[j] + kofs, dst + j * 8192);
+            glds16(Wb + wsrc[j] + kofs, dst + 16384 + j * 8192);
+        }
+    };
+
+    // ---- fragments: row r of a 16-row block, chunk lg, swizzled by (r >> 2) & 2
+    const int cofs = ((lg ^ ((lrow >> 2) & 2)) << 4);
+    const int aoff = (wm * 128 + lrow) * 64 + cofs;
+    const int woff = 16384 + (wn * 64 + lrow) * 64 + cofs;
+    auto read = [&](int t, vec8 (&fa)[FM], vec8 (&fw)[FN]) {
+        const unsigned char* base = smem + (t % NS) * STAGE;
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) fa[fm] = *(const vec8*)(base + aoff + fm * 1024);
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn) fw[fn] = *(const vec8*)(base + woff + fn * 1024);
+    };
+    auto mfmas = [&](const vec8 (&fa)[FM], const vec8 (&fw)[FN]) {
+#pragma unroll
+        for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(fw[fn], fa[fm], acc[fn][fm]);
+    };
+    // one step: 32 MFMAs on (fa, fw) with the next step's copies and fragment reads interleaved
+    auto interleave = [&](bool issue) {
+        if (issue) {
+#pragma unroll
+            for (int i = 0; i < LPS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (glds)
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+            }
+#pragma unroll
+            for (int i = 0; i < FM + FN - LPS; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, FM * FN - (FM + FN) - LPS, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < FM + FN; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, FM * FN - (FM + FN), 0);
+        }
+    };
+
+    const int nk = a.K >> 5;  // even (K % 64 == 0)
+    // prologue: stages 0 .. NS-2 in flight, wait for stage 0 (own copies), publish
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < nk) stage(s);
+    vm_wait_le<LPS>(LPS * min(NS - 2, nk - 1));
+    __builtin_amdgcn_s_barrier();
+    vec8 fa0[FM], fw0[FN], fa1[FM], fw1[FN];
+    read(0, fa0, fw0);
+
+    // steady state: step t waits for stage t+1 (NS - 3 younger stages stay in flight), passes the
+    // barrier (stage t+1 visible; every wave done reading stage t-1), refills stage t-1's buffer
+    // with stage t+NS-1, reads stage t+1's fragments and runs stage t's MFMAs
+    const int nmain = nk - (NS - 1);  // steps that issue a copy; even
+    int t = 0;
+#define CLIPVIT_DEEP_STEP(FA, FW, GA, GW, ISSUE, RD, VMC)                         \
+    {                                                                           \
+        VMC;                                                                    \
+        __builtin_amdgcn_s_waitcnt(0xC07F); /* lgkmcnt(0): FA/FW landed */     \
+        __builtin_amdgcn_s_barrier();                                           \
+        if (ISSUE) stage(t + NS - 1);                                           \
+        if (RD) read(t + 1, GA, GW);                                            \
+        mfmas(FA, FW);                                                          \
+        interleave(ISSUE);                                                      \
+        ++t;                                                                    \
+    }
+    for (; t < nmain;) {
+        CLIPVIT_DEEP_STEP(fa0, fw0, fa1, fw1, true, true, vm_wait<LPS * (NS - 3)>());
+        CLIPVIT_DEEP_STEP(fa1, fw1, fa0, fw0, true, true, vm_wait<LPS * (NS - 3)>());
+    }
+    for (; t < nk;) {  // tail: nothing left to issue; NS - 1 (even) steps
+        CLIPVIT_DEEP_STEP(fa0, fw0, fa1, fw1, false, t + 1 < nk,
+                          if (t + 1 < nk) vm_wait_le<LPS>(LPS * min(NS - 3, nk - 2 - t)));
+        CLIPVIT_DEEP_STEP(fa1, fw1, fa0, fw0, false, t + 1 < nk,
+                          if (t + 1 < nk) vm_wait_le<LPS>(LPS * min(NS - 3, nk - 2 - t)));
+    }
+#undef CLIPVIT_DEEP_STEP
+
+    // ---- epilogue: lane owns token m and features n .. n+15 (bias already in acc)
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = m0 + wm * 128 + fm * 16 + lrow;
+        if (m >= a.M) continue;
+        const int n = n0 + wn * 64 + 16 * lg;
+        float v[16];
+#pragma unroll
+        for (int f = 0; f < 4; ++f)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[f][fm][r];
+        if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+        }
+        if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+            uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+            dst[0] = make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                pack2<T>(v[6], v[7]));
+            dst[1] = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
+                                pack2<T>(v[14], v[15]));
+        } else if constexpr (EPI == EPI_RESID) {
+            float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float4 o = dst[i];
+                o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
+                dst[i] = o;
+            }
+        } else if constexpr (EPI == EPI_DISCARD) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s += v[i];
+            if (s == 1.2345e-30f) ((float*)a.C)[0] = s;  // never taken; keeps the MFMAs live
+        } else {
+            size_t row = (size_t)m;
+            if constexpr (EPI == EPI_PATCH) row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
+            float4* dst = (float4*)((float*)a.C + row * a.ldc + n);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        }
+    }
+}
+
+template <typename T, int NS>
+int launch_deep_t(hipStream_t s, int epi, const GemmArgs& a) {
+    if (a.N % 256) return -1;
+    const int grid = grid_for((a.M + 255) / 256, a.N / 256, a.xcd_n);
+    switch (epi) {
+        case EPI_STORE: gemm_deep_kernel<T, NS, EPI_STORE><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_GELU: gemm_deep_kernel<T, NS, EPI_GELU><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_RESID: gemm_deep_kernel<T, NS, EPI_RESID><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_PATCH: gemm_deep_kernel<T, NS, EPI_PATCH><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_F32: gemm_deep_kernel<T, NS, EPI_F32><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_F32GELU: gemm_deep_kernel<T, NS, EPI_F32GELU><<<grid, 512, 0, s>>>(a); return 0;
+        case EPI_DISCARD: gemm_deep_kernel<T, NS, EPI_DISCARD><<<grid, 512, 0, s>>>(a); return 0;
+    }
+    return -1;
+}
+
+template <typename T>
+int launch_deep_dt(hipStream_t s, int epi, const GemmArgs& a, int variant) {
+    switch (variant) {
+        case 70: return launch_deep_t<T, 5>(s, epi, a);
+        case 71: return launch_deep_t<T, 3>(s, epi, a);
+    }
+    return -1;
+}
+
+}  // namespace
+
+// Deep-ring 256x256 GEMM variants 70 (5-stage ring) and 71 (3-stage ring).
+int launch_gemm_deep(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
+    if (a.K % 64 != 0 || a.M <= 0) return -1;
+    if (dtype == 2) return launch_deep_dt<F16>(s, epi, a, variant);
+    return launch_deep_dt<BF16>(s, epi, a, variant);
+}
+
+}  // namespace clipvit

@@ -27,9 +27,11 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 
 
 # variant = 100 * xcd_partition + tile kernel (include/clipvit.h); 2xx = 4x2 XCD tile partition
-VARIANTS = list(range(1, 16)) + [21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 34, 208, 213, 221, 222, 230]
-N128 = (1, 2, 6, 7, 10, 11, 12, 13, 22, 26)
-N256 = (3, 5, 8, 9, 14, 15, 21, 23, 24, 25, 27, 28, 29, 30, 31, 34)
+VARIANTS = list(range(1, 16)) + [21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 34, 40, 41, 42, 43,
+                                  50, 51, 52, 53, 70, 71, 208, 213, 221, 222, 230, 250, 251, 252, 270]
+N128 = (1, 2, 6, 7, 10, 11, 12, 13, 22, 26, 42, 43, 52)
+N256 = (3, 5, 8, 9, 14, 15, 21, 23, 24, 25, 27, 28, 29, 30, 31, 34, 40, 41, 50, 51, 53, 70, 71)
+PERSIST = (40, 41, 42, 43)  # persistent store-overlapped kernels (gemm_ps.hip)
 DEFER = (30, 31, 34)  # persistent deferred-epilogue kernels: 16-bit outputs, bias, K >= 640
 
 
@@ -114,6 +116,39 @@ def test_gemm_defer_identity_and_gelu(gpu, variant, dtype):
     ref = _ref_gemm(A, W, bias, 1)
     err = (C - ref).abs().max().item() / ref.abs().max().item()
     assert err < _tol(variant, dtype), err
+
+
+@pytest.mark.parametrize("variant", PERSIST + (50, 51, 52, 53, 250, 70, 71, 270))
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_persistent_16bit_and_resid(gpu, variant, dtype):
+    """Persistent kernels: exact identity with 16-bit outputs (bias staged in LDS and used as
+    the accumulator's initial value), several tiles per workgroup with ragged M for the
+    16-bit STORE / GELU epilogues (stores left in flight across k-steps) and the fp32
+    residual epilogue."""
+    K, N = 768, 512
+    A = torch.eye(K, device=gpu).to(dtype)
+    W = (torch.arange(N * K, device=gpu, dtype=torch.float32).reshape(N, K) % 251) / 8.0
+    C = E.gemm_test(A, W, torch.zeros(N, device=gpu), epi=10, variant=variant)
+    assert torch.equal(C, W.to(dtype).float().t()), variant
+    g = torch.Generator(device=gpu).manual_seed(11)
+    M = 12800 + 37
+    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
+    W = torch.randn(3072, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(3072, device=gpu, generator=g)
+    tol = 8e-3 if dtype == torch.bfloat16 else 2e-3
+    for epi in (10, 11):
+        C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
+        ref = _ref_gemm(A, W, bias, epi - 10)
+        err = (C - ref).abs().max().item() / ref.abs().max().item()
+        assert err < tol, (epi, err)
+    W = torch.randn(768, 3072, device=gpu, generator=g) * 0.05
+    A = torch.randn(M, 3072, device=gpu, generator=g).to(dtype)
+    if 768 % (256 if variant % 100 in N256 else 128) == 0:
+        C0 = torch.randn(M, 768, device=gpu, generator=g)
+        C = E.gemm_test(A, W, bias[:768], epi=2, variant=variant, C=C0.clone())
+        ref = _ref_gemm(A, W, bias[:768], 2, C0)
+        err = (C - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-3, err
 
 
 def _ref_attention(qkv, B, N, H):

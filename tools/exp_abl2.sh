@@ -1,0 +1,10 @@
+#!/bin/bash
+set -o pipefail
+mkdir -p gpurun_out
+C=""
+for shape in "12800,2304,768" "12800,3072,768" "4096,4096,4096"; do
+  for v in 8 64 63 15 65 66 16; do C="$C;$shape,4,$v"; done
+done
+C=${C#;}
+timeout -k 10 200 python -u tools/gemm_multi.py "$C" 30 > gpurun_out/abl2_timing.txt 2>&1 || { echo "timing failed"; tail gpurun_out/abl2_timing.txt; exit 1; }
+cat gpurun_out/abl2_timing.txt

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Persistent GEMM experiment: kernel tests, then timing of every role with old vs new variants.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -k gemm -x -q --timeout 120 --timeout-method thread > gpurun_out/ps_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/ps_tests.log; exit 1; }
+tail -2 gpurun_out/ps_tests.log
+C=""
+for v in 208 40 41 43; do C="$C;12800,2304,768,0,$v"; done
+for v in 221 40 41 42 43; do C="$C;12800,768,768,2,$v"; done
+for v in 213 40 41 42 43; do C="$C;12800,3072,768,1,$v"; done
+for v in 221 40 41 42 43; do C="$C;12800,768,3072,2,$v"; done
+C=${C#;}
+timeout -k 10 200 python -u tools/gemm_multi.py "$C" 30 > gpurun_out/ps_timing.txt 2>&1 || { echo "timing failed"; tail gpurun_out/ps_timing.txt; exit 1; }
+# second round, same process order reversed for drift check
+timeout -k 10 200 python -u tools/gemm_multi.py "$C" 30 >> gpurun_out/ps_timing.txt 2>&1
+cat gpurun_out/ps_timing.txt
