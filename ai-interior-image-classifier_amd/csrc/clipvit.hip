@@ -478,7 +478,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (c.width % 256 || c.width < 512 || c.width > 1280)
         FAIL(CLIPVIT_E_INVALID, "width must be a multiple of 256 in [512, 1280]");
     if (c.heads * 64 != c.width) FAIL(CLIPVIT_E_INVALID, "heads * 64 must equal width");
-    if (c.embed_dim % 64 || c.embed_dim <= 0) FAIL(CLIPVIT_E_INVALID, "embed_dim % 64 != 0");
+    if (c.embed_dim % 128 || c.embed_dim <= 0 || c.embed_dim > 1280)
+        FAIL(CLIPVIT_E_INVALID, "embed_dim must be a multiple of 128 in [128, 1280]");
     if (c.compute_dtype != CLIPVIT_BF16 && c.compute_dtype != CLIPVIT_F16 && c.compute_dtype != CLIPVIT_MXFP8)
         FAIL(CLIPVIT_E_INVALID, "compute_dtype must be BF16, F16 or MXFP8");
     if (c.layers <= 0 || c.max_batch <= 0) FAIL(CLIPVIT_E_INVALID, "layers/max_batch must be > 0");

@@ -7,36 +7,178 @@
 // T rows are the cached, already L2-normalised text features (main.py:179-182, 296-311); the
 // library keeps them transposed (Tt [E][Cpad]) so column tiles load coalesced.
 //
-// Both matrix products are small (B x 768 x 512 and B x 512 x 437): each workgroup computes a
-// 16-image x 64-column tile, streaming the weight operand through LDS in 64-deep chunks with
-// float4 loads (no per-iteration global-load latency), 4 images x 1 column per thread.
+// These kernels move a few MB and do ~0.3 GFLOP per batch of 256, so they are bound by latency,
+// not bandwidth (the first version ran 134 us per batch, measured: one global round trip per
+// 64-deep chunk, three passes over every LayerNorm row, and 18 serially dependent cross-lane
+// shuffles per top-k slot on one wave per image). Here:
+//  * both products (B x D x E and B x E x C) use 16-image x 64-column tiles whose weight chunks
+//    are prefetched into registers two chunks ahead of the one being multiplied from LDS;
+//  * a row (LayerNorm input, feature vector) is loaded with all its loads in flight at once and
+//    reduced from registers;
+//  * softmax + top-k runs one wave per (image, segment), all segments of an image in parallel.
+// Per-image results never depend on the batch size or the image's position in it.
 #include "common.h"
 
 namespace clipvit {
 
-constexpr int HR = 16;   // images per workgroup
-constexpr int HK = 64;   // reduction chunk
+constexpr int HR = 16;     // images per workgroup
+constexpr int HK = 128;    // reduction chunk (rows of the weight operand per LDS fill)
+constexpr int HMAXD = 20;  // max row length / 64 held in registers (width <= 1280)
 
-// acc[i] += sum_k X[ib + i][k] * W[k][col]  for k in [0, K), X in LDS [HR][K], W global [K][ldw]
-__device__ __forceinline__ void tile_accumulate(const float* __restrict__ xs, int K,
-                                                const float* __restrict__ W, int ldw, int col0,
-                                                float* ws, float (&acc)[4], int tid) {
-    const int tx = tid & 63, ib = (tid >> 6) * 4;
-    for (int k0 = 0; k0 < K; k0 += HK) {
-        __syncthreads();
-        // 64 x 64 chunk of W: thread loads 4 float4 (rows k0 + (tid >> 4) + 16 j, cols 4 (tid & 15))
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int r = (tid >> 4) + 16 * j, c = (tid & 15) * 4;
-            *(float4*)(ws + r * 68 + c) = *(const float4*)(W + (size_t)(k0 + r) * ldw + col0 + c);
+// Stage rows [b0, b0 + 16) of a [*, ld] fp32 matrix (row stride `stride` floats) into LDS
+// [16][n], optionally LayerNorm-ed (gamma, beta) or L2-normalised; one wave per row, all of a
+// row's loads issued before any is used. Rows >= B are zero.
+template <int MODE>  // 0 LayerNorm, 1 L2 normalise
+__device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t stride, int b0, int B,
+                                           int n, const float* __restrict__ gm,
+                                           const float* __restrict__ bt, float* dst,
+                                           float* __restrict__ norm_out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nv = n >> 6;
+    for (int i = wave; i < HR; i += 4) {
+        const int b = b0 + i;
+        float* d = dst + i * (n + 4);  // rows padded by 4 floats: the product's 4 image reads hit distinct banks
+        if (b >= B) {
+            for (int c = lane; c < n; c += 64) d[c] = 0.f;
+            continue;
         }
-        __syncthreads();
-#pragma unroll 16
-        for (int k = 0; k < HK; ++k) {
-            const float w = ws[k * 68 + tx];
+        const float* r = src + (size_t)b * stride;
+        float v[HMAXD];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[i] += xs[(ib + i) * K + k0 + k] * w;
+        for (int j = 0; j < HMAXD; ++j) {  // unconditional loads (clamped address), then select
+            const float t = r[lane + 64 * min(j, nv - 1)];
+            v[j] = j < nv ? t : 0.f;
         }
+        if constexpr (MODE == 0) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < HMAXD; ++j) s += v[j];
+            const float mean = wave_sum(s) / n;
+            float q = 0.f;
+#pragma unroll
+            for (int j = 0; j < HMAXD; ++j)
+                if (j < nv) q += (v[j] - mean) * (v[j] - mean);
+            const float rstd = rsqrtf(wave_sum(q) / n + 1e-5f);
+#pragma unroll
+            for (int j = 0; j < HMAXD; ++j)
+                if (j < nv) {
+                    const int c = lane + 64 * j;
+                    d[c] = (v[j] - mean) * rstd * gm[c] + bt[c];
+                }
+        } else {
+            float q = 0.f;
+#pragma unroll
+            for (int j = 0; j < HMAXD; ++j) q += v[j] * v[j];
+            const float inv = 1.0f / sqrtf(wave_sum(q));
+#pragma unroll
+            for (int j = 0; j < HMAXD; ++j)
+                if (j < nv) {
+                    const int c = lane + 64 * j;
+                    d[c] = v[j] * inv;
+                    if (norm_out) norm_out[(size_t)b * n + c] = v[j] * inv;
+                }
+        }
+    }
+}
+
+// P = xs[16][K] @ W[K][col0 .. col0 + 64)  (K % 128 == 0), xs in LDS (row stride K + 4) staged
+// by `stage()`, which runs while the first two weight chunks are in flight. Weight chunks
+// (128 x 64) go global -> registers two chunks ahead of the multiply, registers -> LDS ws. Wave
+// w multiplies k-rows [32 w, 32 w + 32) of every chunk into a full 16 x 64 partial tile (lane:
+// images 4 (lane >> 4) .. + 3, columns 4 (lane & 15) .. + 3); the four partials are summed in a
+// fixed order at the end. On return red[i] holds output (image tid >> 4, columns 4 (tid & 15) + i).
+template <typename Stage>
+__device__ __forceinline__ void tile_product(const float* xs, int K, const float* __restrict__ W, int ldw,
+                                             int col0, float* ws, float (&red)[4], int tid, Stage&& stage) {
+    const int lane = tid & 63, wave = tid >> 6;
+    const int ig = lane >> 4, cg = lane & 15;
+    const int lr = tid >> 4, lc = (tid & 15) * 4;
+    const int nc = K / HK;
+    const int xstride = K + 4;
+    float acc[4][4] = {};
+    // two register chunks of 8 float4 (named scalars: an array here ends up in scratch)
+    float4 a0, a1, a2, a3, a4, a5, a6, a7, b0, b1, b2, b3, b4, b5, b6, b7;
+    const size_t l16 = (size_t)16 * ldw;
+#define HEAD_LOAD(x0, x1, x2, x3, x4, x5, x6, x7, k0)                      \
+    {                                                                      \
+        const float* p_ = W + (size_t)((k0) + lr) * ldw + col0 + lc;       \
+        x0 = *(const float4*)p_;                                           \
+        x1 = *(const float4*)(p_ + l16);                                   \
+        x2 = *(const float4*)(p_ + 2 * l16);                               \
+        x3 = *(const float4*)(p_ + 3 * l16);                               \
+        x4 = *(const float4*)(p_ + 4 * l16);                               \
+        x5 = *(const float4*)(p_ + 5 * l16);                               \
+        x6 = *(const float4*)(p_ + 6 * l16);                               \
+        x7 = *(const float4*)(p_ + 7 * l16);                               \
+    }
+#define HEAD_PUT(x0, x1, x2, x3, x4, x5, x6, x7)                           \
+    {                                                                      \
+        float* q_ = ws + lr * 68 + lc;                                     \
+        *(float4*)q_ = x0;                                                 \
+        *(float4*)(q_ + 16 * 68) = x1;                                     \
+        *(float4*)(q_ + 32 * 68) = x2;                                     \
+        *(float4*)(q_ + 48 * 68) = x3;                                     \
+        *(float4*)(q_ + 64 * 68) = x4;                                     \
+        *(float4*)(q_ + 80 * 68) = x5;                                     \
+        *(float4*)(q_ + 96 * 68) = x6;                                     \
+        *(float4*)(q_ + 112 * 68) = x7;                                    \
+    }
+    auto mul = [&](int k0) {
+        const float* xr = xs + (4 * ig) * xstride + k0 + 32 * wave;
+        const float* wr = ws + (32 * wave) * 68 + 4 * cg;
+#pragma unroll 2
+        for (int k = 0; k < 32; k += 4) {
+            float4 x[4], w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = *(const float4*)(xr + i * xstride + k);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = *(const float4*)(wr + (k + j) * 68);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[i][0] += xv[j] * w[j].x;
+                    acc[i][1] += xv[j] * w[j].y;
+                    acc[i][2] += xv[j] * w[j].z;
+                    acc[i][3] += xv[j] * w[j].w;
+                }
+            }
+        }
+    };
+    HEAD_LOAD(a0, a1, a2, a3, a4, a5, a6, a7, 0);
+    if (nc > 1) HEAD_LOAD(b0, b1, b2, b3, b4, b5, b6, b7, HK);
+    stage();
+    for (int c = 0; c < nc; c += 2) {
+        __syncthreads();  // xs staged (first pass) / previous chunk's reads done
+        HEAD_PUT(a0, a1, a2, a3, a4, a5, a6, a7);
+        __syncthreads();
+        if (c + 2 < nc) HEAD_LOAD(a0, a1, a2, a3, a4, a5, a6, a7, (c + 2) * HK);
+        mul(c * HK);
+        if (c + 1 >= nc) break;
+        __syncthreads();
+        HEAD_PUT(b0, b1, b2, b3, b4, b5, b6, b7);
+        __syncthreads();
+        if (c + 3 < nc) HEAD_LOAD(b0, b1, b2, b3, b4, b5, b6, b7, (c + 3) * HK);
+        mul((c + 1) * HK);
+    }
+#undef HEAD_LOAD
+#undef HEAD_PUT
+    // sum the four per-wave partial tiles (fixed order) through LDS
+    __syncthreads();
+    float* part = ws;  // [4 waves][16 images][64 columns]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        *(float4*)(part + wave * 1024 + (4 * ig + i) * 64 + 4 * cg) =
+            make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+    __syncthreads();
+    const int img = tid >> 4, cq = (tid & 15) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) red[i] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const float4 v = *(const float4*)(part + w * 1024 + img * 64 + cq);
+        red[0] += v.x; red[1] += v.y; red[2] += v.z; red[3] += v.w;
     }
 }
 
@@ -47,39 +189,17 @@ __global__ __launch_bounds__(256) void cls_ln_proj_kernel(const float* __restric
                                                           const float* __restrict__ proj,
                                                           float* __restrict__ f, int B, int N,
                                                           int D, int E) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][D] + [64][68]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][D] + [128][68]
     float* ys = sm;
-    float* ws = sm + HR * D;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * HR;
-    for (int i = wave; i < HR; i += 4) {  // LayerNorm of the CLS rows (one wave per row)
-        const int b = b0 + i;
-        float* yr = ys + i * D;
-        if (b >= B) {
-            for (int c = lane; c < D; c += 64) yr[c] = 0.f;
-            continue;
-        }
-        const float* xr = x + (size_t)b * N * D;  // CLS token = row 0 of the image
-        float s = 0.f;
-        for (int c = lane; c < D; c += 64) s += xr[c];
-        const float mean = wave_sum(s) / D;
-        float q = 0.f;
-        for (int c = lane; c < D; c += 64) {
-            const float d = xr[c] - mean;
-            q += d * d;
-        }
-        const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
-        for (int c = lane; c < D; c += 64) yr[c] = (xr[c] - mean) * rstd * gm[c] + bt[c];
-    }
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int col0 = blockIdx.y * 64;
-    tile_accumulate(ys, D, proj, E, col0, ws, acc, tid);
-    const int ib = wave * 4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int b = b0 + ib + i;
-        if (b < B) f[(size_t)b * E + col0 + lane] = acc[i];
-    }
+    float* ws = sm + HR * (D + 4);
+    const int tid = threadIdx.x;
+    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * 64;
+    float red[4];
+    tile_product(ys, D, proj, E, col0, ws, red, tid, [&]() {  // CLS token = row 0 of each image
+        stage_rows<0>(x, (size_t)N * D, b0, B, D, gm, bt, ys, nullptr);
+    });
+    const int b = b0 + (tid >> 4);
+    if (b < B) *(float4*)(f + (size_t)b * E + col0 + (tid & 15) * 4) = make_float4(red[0], red[1], red[2], red[3]);
 }
 
 // grid (ceil(B/16), Cpad/64), 256 threads.
@@ -88,56 +208,37 @@ __global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ f
                                                      float* __restrict__ emb_norm,
                                                      float* __restrict__ logits, int B, int E,
                                                      int C, int Cpad) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][E] + [64][68]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][E] + [128][68]
     float* fs = sm;
-    float* ws = sm + HR * E;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int b0 = blockIdx.x * HR;
-    for (int i = wave; i < HR; i += 4) {
-        const int b = b0 + i;
-        float* fr = fs + i * E;
-        if (b >= B) {
-            for (int c = lane; c < E; c += 64) fr[c] = 0.f;
-            continue;
-        }
-        const float* src = f + (size_t)b * E;
-        float q = 0.f;
-        for (int c = lane; c < E; c += 64) q += src[c] * src[c];
-        const float inv = 1.0f / sqrtf(wave_sum(q));
-        for (int c = lane; c < E; c += 64) {
-            const float v = src[c] * inv;
-            fr[c] = v;
-            if (emb_norm && blockIdx.y == 0) emb_norm[(size_t)b * E + c] = v;
-        }
-    }
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    const int col0 = blockIdx.y * 64;
-    tile_accumulate(fs, E, Tt, Cpad, col0, ws, acc, tid);
-    const int c = col0 + lane, ib = wave * 4;
-    if (c < C) {
+    float* ws = sm + HR * (E + 4);
+    const int tid = threadIdx.x;
+    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * 64;
+    float red[4];
+    tile_product(fs, E, Tt, Cpad, col0, ws, red, tid, [&]() {
+        stage_rows<1>(f, (size_t)E, b0, B, E, nullptr, nullptr, fs, blockIdx.y == 0 ? emb_norm : nullptr);
+    });
+    const int b = b0 + (tid >> 4), c = col0 + (tid & 15) * 4;
+    if (b < B) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int b = b0 + ib + i;
-            if (b < B) logits[(size_t)b * C + c] = 100.0f * acc[i];
-        }
+        for (int i = 0; i < 4; ++i)
+            if (c + i < C) logits[(size_t)b * C + c + i] = 100.0f * red[i];
     }
 }
 
-// One wave per image; the image's logits row is staged in LDS once, then every segment's
-// max / sum / top-min(5, n) (ties -> lower index, like a stable sort) runs from LDS.
-constexpr int SM_WAVES = 4;
+// One workgroup per image, one wave per label segment (segments beyond the wave count loop):
+// the image's logits row is staged in LDS, then each wave computes its segment's max / sum /
+// probabilities and top-min(5, n) (ties -> lower index, like a stable sort) from LDS.
+constexpr int SM_WAVES = 8;
 __global__ __launch_bounds__(64 * SM_WAVES) void seg_softmax_topk_kernel(
     const float* __restrict__ logits, float* __restrict__ probs, int* __restrict__ top_idx,
     float* __restrict__ top_prob, const int* __restrict__ seg_off, int nseg, int B, int C) {
-    extern __shared__ __attribute__((aligned(16))) float rows[];  // [SM_WAVES][C]
+    extern __shared__ __attribute__((aligned(16))) float lr[];  // [C]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b = blockIdx.x * SM_WAVES + wave;
-    if (b >= B) return;
-    float* lr = rows + wave * C;
+    const int b = blockIdx.x;
     const float* src = logits + (size_t)b * C;
-    for (int c = lane; c < C; c += 64) lr[c] = src[c];
-    __builtin_amdgcn_s_waitcnt(0);  // own wave's LDS writes visible to its own later reads
-    for (int sg = 0; sg < nseg; ++sg) {
+    for (int c = threadIdx.x; c < C; c += 64 * SM_WAVES) lr[c] = src[c];
+    __syncthreads();
+    for (int sg = wave; sg < nseg; sg += SM_WAVES) {
         const int s0 = seg_off[sg], s1 = seg_off[sg + 1], n = s1 - s0;
         float m = -INFINITY;
         for (int c = s0 + lane; c < s1; c += 64) m = fmaxf(m, lr[c]);
@@ -186,7 +287,7 @@ void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const flo
                                                  160 * 1024) == hipSuccess;
     (void)attr;
     dim3 grid((B + HR - 1) / HR, E / 64), block(256);
-    const size_t lds = (HR * D + 64 * 68) * sizeof(float);
+    const size_t lds = (HR * (D + 4) + HK * 68) * sizeof(float);
     cls_ln_proj_kernel<<<grid, block, lds, s>>>(x, g, b, proj, f, B, N, D, E);
 }
 
@@ -197,15 +298,14 @@ void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_no
                                                  160 * 1024) == hipSuccess;
     (void)attr;
     dim3 grid((B + HR - 1) / HR, Cpad / 64), block(256);
-    const size_t lds = (HR * E + 64 * 68) * sizeof(float);
+    const size_t lds = (HR * (E + 4) + HK * 68) * sizeof(float);
     logits_kernel<<<grid, block, lds, s>>>(f, Tt, emb_norm, logits, B, E, C, Cpad);
 }
 
 void launch_seg_softmax_topk(hipStream_t s, const float* logits, float* probs, int* top_idx,
                              float* top_prob, const int* seg_off, int nseg, int B, int C) {
-    const int blocks = (B + SM_WAVES - 1) / SM_WAVES;
-    seg_softmax_topk_kernel<<<blocks, 64 * SM_WAVES, SM_WAVES * C * sizeof(float), s>>>(
-        logits, probs, top_idx, top_prob, seg_off, nseg, B, C);
+    seg_softmax_topk_kernel<<<B, 64 * SM_WAVES, C * sizeof(float), s>>>(logits, probs, top_idx, top_prob,
+                                                                      seg_off, nseg, B, C);
 }
 
 }  // namespace clipvit
