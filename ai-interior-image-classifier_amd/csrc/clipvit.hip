@@ -126,9 +126,10 @@ struct clipvit_handle {
     std::vector<int> seg_host;
     std::mutex mu;
     std::vector<Workspace*> pool;
-    // GEMM tile variants per role (qkv, out, fc, proj, patch), from tools/gemm_tune.py sweeps
-    // on MI355X (profiles/); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
-    int var[5] = {8, 21, 13, 21, 21};
+    // GEMM tile variants per role (qkv, out, fc, proj, patch), from in-model sweeps on MI355X
+    // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
+    // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles)
+    int var[5] = {8, 22, 13, 22, 22};
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
     int xcd[5] = {2, 2, 2, 2, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
@@ -142,6 +143,10 @@ struct clipvit_handle {
     // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
     uint64_t mx8_skip = 0;
     bool q8_layer(int i) const { return mx8 && !((mx8_skip >> i) & 1); }
+    // residual adds of out_proj / c_proj: true = the GEMM stores its 16-bit branch output y and
+    // the following LayerNorm kernel does x += y (fp16 default; CLIPVIT_RESID16=0/1 overrides);
+    // false = fp32 read-modify-write of x in the GEMM epilogue
+    bool resid16 = false;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -365,27 +370,43 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
                     B, N, D);
     if (prof) prof->mark(s, F_EMBED);
+    // 16-bit residual branch outputs (resid16) reuse the qkv buffer: qkv is dead once attention
+    // has read it, and the branch output of c_proj is consumed before the next QKV GEMM
+    void* y = w->qkv;
     for (int i = 0; i < h->cfg.layers; ++i) {
         const LayerW& ly = h->layers[i];
+        const bool last = i + 1 == h->cfg.layers;
         if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (prof) prof->mark(s, F_ATTN);
-        if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT)))
-            return rc;
-        if (prof) prof->mark(s, F_OUT);
-        launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
+        if (h->resid16) {
+            if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT))) return rc;
+            if (prof) prof->mark(s, F_OUT);
+            launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
+        } else {
+            if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT))) return rc;
+            if (prof) prof->mark(s, F_OUT);
+            launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
+        }
         if (prof) prof->mark(s, F_LN);
         if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC)))
             return rc;
         if (prof) prof->mark(s, F_FC);
-        if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)))
-            return rc;
-        if (prof) prof->mark(s, F_PROJ);
-        if (i + 1 < h->cfg.layers) {
-            launch_layernorm(s, h->dt, w->x, w->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+        if (h->resid16 && !last) {
+            if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, y, M, D, 4 * D, D, R_PROJ))) return rc;
+            if (prof) prof->mark(s, F_PROJ);
+            launch_add_layernorm(s, h->dt, w->x, y, w->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
+        } else {
+            if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)))
+                return rc;
+            if (prof) prof->mark(s, F_PROJ);
+            if (!last) {
+                launch_layernorm(s, h->dt, w->x, w->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+                if (prof) prof->mark(s, F_LN);
+            }
         }
     }
     launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
@@ -499,6 +520,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->Kp = (h->K3 + 63) / 64 * 64;
     h->mx8 = c.compute_dtype == CLIPVIT_MXFP8;
     h->dt = h->mx8 ? CLIPVIT_BF16 : c.compute_dtype;  // 16-bit type of everything not MX-fp8
+    h->resid16 = !h->mx8 && h->dt == CLIPVIT_F16;
+    if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;

@@ -205,6 +205,8 @@ void launch_quant_mx8(hipStream_t s, int in_dtype, const void* src, unsigned cha
 void launch_fill_random_mx8(hipStream_t s, unsigned char* q, unsigned char* sq, size_t n, unsigned seed);
 void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, unsigned char* sq,
                             int N, int K, int Kp);
+void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
+                          const float* b, int rows, int D);
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
                          const float* g, const float* b, int rows, int D);
 void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,

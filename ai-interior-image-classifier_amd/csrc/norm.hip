@@ -197,6 +197,38 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
+// x[row] += y[row] (16-bit branch output of out_proj / c_proj); h[row] = LayerNorm(x[row]).
+// Moves the residual add out of the GEMM epilogue (which then only stores y): the GEMM no
+// longer reads x, and this kernel streams x, y -> x, h in one pass.
+template <typename T, int V>
+__global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, const u16* __restrict__ y,
+                                                            u16* __restrict__ h, const float* __restrict__ gm,
+                                                            const float* __restrict__ bt, int rows) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    constexpr int D = 256 * V;
+    float* xr = x + (size_t)row * D;
+    const u16* yr = y + (size_t)row * D;
+    float4 v[V];
+    uint2 w[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
+        w[i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i].x += T::to_f32((u16)(w[i].x & 0xffff));
+        v[i].y += T::to_f32((u16)(w[i].x >> 16));
+        v[i].z += T::to_f32((u16)(w[i].y & 0xffff));
+        v[i].w += T::to_f32((u16)(w[i].y >> 16));
+        *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    }
+    ln_row<V>(v, gm, bt, lane, (float)D);
+    store_row16<T, V>(h + (size_t)row * D, v, lane);
+}
+
 #define DISPATCH_V(D, ...)                          \
     switch ((D) / 256) {                            \
         case 2: { constexpr int V = 2; __VA_ARGS__; } break; \
@@ -230,6 +262,16 @@ void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsign
                          const float* g, const float* b, int rows, int D) {
     dim3 grid((rows + 3) / 4), block(256);
     DISPATCH_V(D, layernorm_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, g, b, rows));
+}
+
+void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
+                          const float* b, int rows, int D) {
+    dim3 grid((rows + 3) / 4), block(256);
+    if (dtype == 2) {
+        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, (u16*)h, g, b, rows));
+    } else {
+        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, (u16*)h, g, b, rows));
+    }
 }
 
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
