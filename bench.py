@@ -179,7 +179,7 @@ def main():
         "config": {"workload": f"{cfg.name} + merged LoRA r={a.lora_rank} classify (encode_image + cosine head over {N_CLASSES} labels, 6 segments)",
                    "image_size": cfg.image_size, "per_gpu_batch": a.batch, "global_batch": a.batch * world,
                    "parallelism": f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else "")},
-        "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj+residual)",
+        "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj)",
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),
                      "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(mlp_ms, 5),
