@@ -32,7 +32,9 @@ __device__ __forceinline__ void vm_wait_le(int n) {  // s_waitcnt vmcnt(n), n <=
     else vm_wait<0>();
 }
 
-template <typename T, int NS, int EPI>
+// ABL (timing-only ablation builds, results wrong): bit0 no global->LDS loads, bit1 no LDS
+// fragment reads, bit2 no MFMAs.
+template <typename T, int NS, int EPI, int ABL = 0>
 __global__ __launch_bounds__(512) void gemm_deep_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     static_assert(NS == 3 || NS == 5, "ring depth: NS - 1 must be even (loop unrolled by 2)");
@@ -80,6 +82,7 @@ __global__ __launch_bounds__(512) void gemm_deep_kernel(GemmArgs a) {
         wsrc[j] = (size_t)(n0 + row) * ldb + c * 16;
     }
     auto stage = [&](int t) {
+        if constexpr (ABL & 1) return;
         unsigned char* dst = smem + (t % NS) * STAGE + wave * 1024;
         const size_t kofs = (size_t)t * 64;
 #pragma unroll
@@ -94,6 +97,13 @@ __global__ __launch_bounds__(512) void gemm_deep_kernel(GemmArgs a) {
     const int aoff = (wm * 128 + lrow) * 64 + cofs;
     const int woff = 16384 + (wn * 64 + lrow) * 64 + cofs;
     auto read = [&](int t, vec8 (&fa)[FM], vec8 (&fw)[FN]) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) asm volatile("" : "=v"(fa[fm]));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) asm volatile("" : "=v"(fw[fn]));
+            return;
+        }
         const unsigned char* base = smem + (t % NS) * STAGE;
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) fa[fm] = *(const vec8*)(base + aoff + fm * 1024);
@@ -101,6 +111,13 @@ __global__ __launch_bounds__(512) void gemm_deep_kernel(GemmArgs a) {
         for (int fn = 0; fn < FN; ++fn) fw[fn] = *(const vec8*)(base + woff + fn * 1024);
     };
     auto mfmas = [&](const vec8 (&fa)[FM], const vec8 (&fw)[FN]) {
+        if constexpr (ABL & 4) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) asm volatile("" ::"v"(fa[fm]));
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn) asm volatile("" ::"v"(fw[fn]));
+            return;
+        }
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
@@ -235,6 +252,14 @@ int launch_deep_dt(hipStream_t s, int epi, const GemmArgs& a, int variant) {
     switch (variant) {
         case 70: return launch_deep_t<T, 5>(s, epi, a);
         case 71: return launch_deep_t<T, 3>(s, epi, a);
+        case 72: case 73: case 74: {  // ablations of 70 (timing only): loads only / MFMA only / no MFMA
+            if (a.N % 256) return -1;
+            const int grid = grid_for((a.M + 255) / 256, a.N / 256, a.xcd_n);
+            if (variant == 72) gemm_deep_kernel<T, 5, EPI_DISCARD, 6><<<grid, 512, 0, s>>>(a);
+            else if (variant == 73) gemm_deep_kernel<T, 5, EPI_DISCARD, 3><<<grid, 512, 0, s>>>(a);
+            else gemm_deep_kernel<T, 5, EPI_DISCARD, 4><<<grid, 512, 0, s>>>(a);
+            return 0;
+        }
     }
     return -1;
 }
