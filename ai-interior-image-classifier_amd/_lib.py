@@ -22,7 +22,7 @@ EXPORTS = (
     "clipvit_encode_image", "clipvit_classify", "clipvit_text_shape", "clipvit_destroy",
     "clipvit_last_error", "clipvit_abi_version", "clipvit_gemm_test", "clipvit_attention_test",
     "clipvit_profile_forward", "clipvit_gemm_bench", "clipvit_quant_mx8_test",
-    "clipvit_gemm_mx8_test",
+    "clipvit_gemm_mx8_test", "clipvit_preprocess", "clipvit_resample_plan",
 )
 
 
@@ -41,6 +41,10 @@ class Config(ctypes.Structure):
 class Tensor(ctypes.Structure):
     _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.POINTER(ctypes.c_float)),
                 ("ndim", ctypes.c_int), ("shape", ctypes.c_int64 * 4)]
+
+
+class Image(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_int64), ("width", ctypes.c_int), ("height", ctypes.c_int)]
 
 
 class Lora(ctypes.Structure):
@@ -82,6 +86,9 @@ def lib() -> ctypes.CDLL:
             "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),
             "clipvit_gemm_bench": (i, [i, i, i, i, i, i, i, p_f]),
+            "clipvit_preprocess": (i, [vp, vp, ctypes.POINTER(Image), i, i, i, vp]),
+            "clipvit_resample_plan": (i, [i, i, ctypes.POINTER(i), ctypes.POINTER(i),
+                                          ctypes.POINTER(ctypes.c_int32), i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -30,7 +30,7 @@ from . import labels as L
 from .config import ViTConfig, get_config
 from .engine import VisionEngine
 from .lora import load_lora_checkpoint, vision_adapters_from_checkpoint
-from .preprocess import load_image, preprocess_batch
+from .preprocess import load_image, preprocess_batch, preprocess_batch_gpu
 from .weights import synthetic_state_dict
 
 
@@ -52,7 +52,8 @@ class InteriorAnalyzer:
                  dataset_json: str | Path = "interior_dataset.json",
                  text_features: dict[str, np.ndarray] | np.ndarray | None = None,
                  categories: dict[str, list[str]] | None = None, max_batch: int = 64,
-                 weights_seed: int = 0):
+                 weights_seed: int = 0, gpu_preprocess: bool = True):
+        self.gpu_preprocess = bool(gpu_preprocess)  # _transform on the GPU (bit-identical)
         self.cfg = model if isinstance(model, ViTConfig) else get_config(model)
         self.engine = VisionEngine(self.cfg, device=device, compute_dtype=compute_dtype,
                                    max_batch=max_batch)
@@ -86,6 +87,13 @@ class InteriorAnalyzer:
                                for s in self.table.segments], axis=0)
 
     # ------------------------------------------------------------------ core batch pass
+    def _pixels(self, images) -> torch.Tensor:
+        """preprocess (main.py:201/438/489) of RGB PIL images: on the GPU by default
+        (clipvit_preprocess), else PIL on host threads; both give the same fp32 bits."""
+        if self.gpu_preprocess:
+            return preprocess_batch_gpu(images, self.cfg.image_size, self.engine.device)
+        return preprocess_batch(images, self.cfg.image_size)
+
     def _run(self, pixels: torch.Tensor):
         out = self.engine.classify(pixels)
         return (out.probs.cpu().numpy(), out.top_idx.cpu().numpy(), out.top_prob.cpu().numpy())
@@ -132,7 +140,7 @@ class InteriorAnalyzer:
         n_px = self.cfg.image_size
         for a in range(0, len(images), batch_size):
             chunk = images[a:a + batch_size]
-            px = preprocess_batch(chunk, n_px)
+            px = self._pixels(chunk)
             probs, tidx, tprob = self._run(px)
             for i in range(len(chunk)):
                 out.append(self._result(probs[i], tidx[i], tprob[i], confidence_threshold, filter_interiors))
@@ -145,7 +153,7 @@ class InteriorAnalyzer:
         if image is None:
             return False, 0.0, "invalid image"                       # main.py:196-197
         try:
-            px = preprocess_batch([image], self.cfg.image_size)
+            px = self._pixels([image])
             probs, _, _ = self._run(px)
             return self._detector(probs[0], confidence_threshold)
         except Exception as e:                                       # main.py:224-226

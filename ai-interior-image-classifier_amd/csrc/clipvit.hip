@@ -23,9 +23,12 @@
 #include "clipvit.h"
 #include "common.h"
 
-using namespace clipvit;
+namespace clipvit {
+// last error of this host thread; shared with preprocess.hip
+thread_local std::string g_err;
+}  // namespace clipvit
 
-static thread_local std::string g_err;
+using namespace clipvit;
 
 #define FAIL(code, msg)        \
     do {                       \

@@ -137,6 +137,32 @@ const char* clipvit_last_error(void);
 /* ABI version compiled into the library (CLIPVIT_ABI_VERSION). */
 int clipvit_abi_version(void);
 
+/* ---- GPU preprocessing ----
+ * Replaces preprocess(img) = clip's _transform(n_px) [3p] at main.py:201, main.py:438,
+ * main.py:489 for images already decoded to RGB (load_image, main.py:119-128):
+ * Resize(n_px, BICUBIC) -> CenterCrop(n_px) -> ToTensor -> Normalize(CLIP mean/std).
+ * The resampling is Pillow's 8-bit fixed-point two-pass convolution, bit-identical to
+ * PIL.Image.resize(BICUBIC) followed by the crop. */
+typedef struct {
+    int64_t offset;   /* byte offset of the image's HWC uint8 RGB pixels in rgb_dev */
+    int width;        /* source width  (pixels) */
+    int height;       /* source height (pixels) */
+} clipvit_image;
+
+/* B images packed in one device byte buffer (each image [height, width, 3] uint8 at its
+ * offset) -> out_dev [B, 3, n_px, n_px] CLIP-normalised pixels of out_dtype (F32, BF16 or
+ * F16), the input clipvit_encode_image / clipvit_classify take. Asynchronous on `stream`;
+ * the image table is staged before the call returns, so `images` may be freed after it. */
+int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit_image* images,
+                       int B, int n_px, int out_dtype, void* out_dev);
+
+/* Host-only: Pillow's resampling plan for one axis (in_size -> out_size, bicubic): *ksize
+ * taps per output; bounds [out_size][2] = (first source index, tap count); kk
+ * [out_size][*ksize] fixed-point weights with 22 fraction bits (kk_cap = capacity of kk in
+ * int32 elements). Identity plan (1 tap, weight 2^22) when in_size == out_size. */
+int clipvit_resample_plan(int in_size, int out_size, int* ksize, int* bounds, int32_t* kk,
+                          int kk_cap);
+
 /* ---- kernel-level entry points (testing / benchmarking of single hot kernels) ----
  * These operate on caller-owned device buffers with the packed layouts documented in
  * DESIGN.md; they are what the per-kernel parity tests and the roofline probe call. */
