@@ -23,6 +23,8 @@ EXPORTS = (
     "clipvit_last_error", "clipvit_abi_version", "clipvit_gemm_test", "clipvit_attention_test",
     "clipvit_profile_forward", "clipvit_gemm_bench", "clipvit_quant_mx8_test",
     "clipvit_gemm_mx8_test", "clipvit_preprocess", "clipvit_resample_plan",
+    "clipvit_text_create", "clipvit_text_load_weights", "clipvit_text_load_lora",
+    "clipvit_encode_text", "clipvit_text_destroy",
 )
 
 
@@ -36,6 +38,11 @@ class Config(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in (
         "image_size", "patch_size", "width", "layers", "heads", "embed_dim", "compute_dtype",
         "max_batch")]
+
+
+class TextConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "width", "layers", "heads", "context", "vocab", "embed_dim", "compute_dtype", "max_batch")]
 
 
 class Tensor(ctypes.Structure):
@@ -86,6 +93,11 @@ def lib() -> ctypes.CDLL:
             "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),
             "clipvit_gemm_bench": (i, [i, i, i, i, i, i, i, p_f]),
+            "clipvit_text_create": (i, [ctypes.POINTER(TextConfig), i, ctypes.POINTER(vp)]),
+            "clipvit_text_load_weights": (i, [vp, ctypes.POINTER(Tensor), ctypes.c_size_t]),
+            "clipvit_text_load_lora": (i, [vp, ctypes.POINTER(Lora), ctypes.c_size_t]),
+            "clipvit_encode_text": (i, [vp, vp, vp, i, i, vp]),
+            "clipvit_text_destroy": (i, [vp]),
             "clipvit_preprocess": (i, [vp, vp, ctypes.POINTER(Image), i, i, i, vp]),
             "clipvit_resample_plan": (i, [i, i, ctypes.POINTER(i), ctypes.POINTER(i),
                                           ctypes.POINTER(ctypes.c_int32), i]),

@@ -49,3 +49,29 @@ def get_config(name: str) -> ViTConfig:
     if name not in MODELS:
         raise ValueError(f"unknown model {name!r}; available: {sorted(MODELS)}")
     return MODELS[name]
+
+
+@dataclass(frozen=True)
+class TextConfig:
+    """OpenAI-CLIP text tower (CLIP.__init__ [3p]: transformer_width/layers/heads,
+    context_length, vocab_size, embed_dim), used by encode_text at main.py:181 / main.py:308.
+    B/32 and B/16 share it; L/14 has width 768, 12 heads, embed 768."""
+    width: int = 512
+    layers: int = 12
+    heads: int = 8
+    context: int = 77
+    vocab: int = 49408
+    embed_dim: int = 512
+
+    def gflop_per_text(self) -> float:
+        N, D = self.context, self.width
+        return (self.layers * (2.0 * N * D * 12 * D + 4.0 * N * N * D) + 2.0 * D * self.embed_dim) / 1e9
+
+
+TEXT_B = TextConfig()
+TEXT_L = TextConfig(width=768, heads=12, embed_dim=768)
+
+
+def text_config_for(vision: ViTConfig, vocab: int = 49408) -> TextConfig:
+    base = TEXT_L if vision.width == 1024 else TEXT_B
+    return TextConfig(base.width, base.layers, base.heads, base.context, vocab, base.embed_dim)

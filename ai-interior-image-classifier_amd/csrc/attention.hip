@@ -23,7 +23,9 @@
 
 namespace clipvit {
 
-template <typename T>
+// CAUSAL (text tower, CLIP.build_attention_mask: -inf above the diagonal): key j is masked
+// for query i < j, and key blocks past the workgroup's last query are skipped.
+template <typename T, bool CAUSAL = false>
 __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ qkv,
                                                         u16* __restrict__ out, int N, int H) {
     typedef typename T::vec8 vec8;
@@ -52,7 +54,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
     float m_run = -INFINITY, l_run = 0.f;
     const float scale = 0.125f;  // 1/sqrt(64)
 
-    const int nkb = (N + 63) >> 6;
+    const int nkb = CAUSAL ? min((N + 63) >> 6, qb + 1) : (N + 63) >> 6;
     for (int kb = 0; kb < nkb; ++kb) {
         __syncthreads();
         {   // cooperative load of 64 keys: thread -> (key = tid>>2, d = 16*(tid&3) .. +15)
@@ -100,7 +102,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int key = kb * 64 + kt * 16 + 4 * g + r;
-                const float v = key < N ? s[kt][r] * scale : -INFINITY;
+                const bool live = key < N && (!CAUSAL || key <= q);
+                const float v = live ? s[kt][r] * scale : -INFINITY;
                 s[kt][r] = v;
                 mloc = fmaxf(mloc, v);
             }
@@ -162,12 +165,19 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
     }
 }
 
-void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H) {
+void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
+                      bool causal) {
     dim3 grid((N + 63) / 64, H, B), block(256);
-    if (dtype == 2)
+    if (causal) {
+        if (dtype == 2)
+            attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (dtype == 2) {
         attention_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    else
+    } else {
         attention_kernel<BF16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    }
 }
 
 }  // namespace clipvit

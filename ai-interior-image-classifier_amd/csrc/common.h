@@ -190,6 +190,41 @@ __host__ __device__ inline int grid_for(int nM, int nN, int xn) {
     return nM * nN;
 }
 
+// Row LayerNorm helpers: one wave per row, D = 64 * 4 * V (V float4 per lane).
+template <int V>
+__device__ __forceinline__ void ln_row(float4 (&v)[V], const float* __restrict__ gm,
+                                       const float* __restrict__ bt, int lane, float D) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    const float mean = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
+        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
+    }
+    const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        const float4 gg = *(const float4*)(gm + c), bb = *(const float4*)(bt + c);
+        v[i].x = v[i].x * rstd * gg.x + bb.x;
+        v[i].y = v[i].y * rstd * gg.y + bb.y;
+        v[i].z = v[i].z * rstd * gg.z + bb.z;
+        v[i].w = v[i].w * rstd * gg.w + bb.w;
+    }
+}
+
+template <typename T, int V>
+__device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int lane) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        *(uint2*)(dst + c) = make_uint2(pack2<T>(v[i].x, v[i].y), pack2<T>(v[i].z, v[i].w));
+    }
+}
+
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
@@ -215,7 +250,8 @@ void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char
 
 void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n);
 
-void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H);
+void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
+                      bool causal = false);
 
 void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, void* acol, int B,
                    int R, int P, int Kp);

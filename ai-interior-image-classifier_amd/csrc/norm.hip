@@ -88,40 +88,7 @@ void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, 
 }
 
 // ---------------------------------------------------------------------------------------
-// Row LayerNorm helpers: one wave per row, D = 64 * 4 * V (V float4 per lane).
-template <int V>
-__device__ __forceinline__ void ln_row(float4 (&v)[V], const float* __restrict__ gm,
-                                       const float* __restrict__ bt, int lane, float D) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
-    const float mean = wave_sum(s) / D;
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-        v[i].x -= mean; v[i].y -= mean; v[i].z -= mean; v[i].w -= mean;
-        q += (v[i].x * v[i].x + v[i].y * v[i].y) + (v[i].z * v[i].z + v[i].w * v[i].w);
-    }
-    const float rstd = rsqrtf(wave_sum(q) / D + 1e-5f);
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-        const int c = (lane + 64 * i) * 4;
-        const float4 gg = *(const float4*)(gm + c), bb = *(const float4*)(bt + c);
-        v[i].x = v[i].x * rstd * gg.x + bb.x;
-        v[i].y = v[i].y * rstd * gg.y + bb.y;
-        v[i].z = v[i].z * rstd * gg.z + bb.z;
-        v[i].w = v[i].w * rstd * gg.w + bb.w;
-    }
-}
-
-template <typename T, int V>
-__device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int lane) {
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-        const int c = (lane + 64 * i) * 4;
-        *(uint2*)(dst + c) = make_uint2(pack2<T>(v[i].x, v[i].y), pack2<T>(v[i].z, v[i].w));
-    }
-}
+// Row LayerNorm helpers ln_row / store_row16: common.h (shared with text.hip).
 
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the

@@ -112,6 +112,28 @@ def vision_adapters_from_checkpoint(ckpt, cfg: ViTConfig, rank: int = 4, alpha: 
     return items, len(bound), missing
 
 
+def text_adapters_from_checkpoint(ckpt, text_layers: int = 12, rank: int = 4, alpha: float = 8.0,
+                                  vision_layers: int = 12):
+    """The same binding (main.py:93-109) for the TEXT tower, where the shipped checkpoints'
+    adapters live (``clip_model.transformer.resblocks.{i}.mlp.{c_fc,c_proj}``): merge items
+    for ``clipvit_text_load_lora`` (targets ``transformer.resblocks.{i}.mlp.*.weight``), plus
+    (loaded, missing). ``attn.out_proj`` adapters are dropped (never executed, see header)."""
+    names = wrapped_lora_param_names(vision_layers, text_layers)
+    bound, missing = bind(ckpt, names)
+    scaling = alpha / rank  # main.py:28
+    items = []
+    for i in range(text_layers):
+        for leaf in LIVE_VISION_LEAVES:
+            base = f"transformer.resblocks.{i}.{leaf}.lora."
+            A, B = bound.get(base + "lora_A"), bound.get(base + "lora_B")
+            if A is None or B is None or not torch.any(B != 0):
+                continue
+            items.append(LoraAdapter(f"transformer.resblocks.{i}.{TARGET_WEIGHT[leaf]}",
+                                     np.ascontiguousarray(A.float().numpy()),
+                                     np.ascontiguousarray(B.float().numpy()), scaling))
+    return items, len(bound), missing
+
+
 def synthetic_adapters(cfg: ViTConfig, rank: int = 8, alpha: float | None = None, seed: int = 1,
                        leaves=("attn.in_proj", "attn.out_proj", "mlp.c_fc", "mlp.c_proj")):
     """BASELINE.json's 'ViT-B/32 + LoRA r=8' (and r=16 for L/14): seeded adapters on every

@@ -59,6 +59,45 @@ def synthetic_state_dict(cfg: ViTConfig, seed: int = 0) -> dict[str, torch.Tenso
     return sd
 
 
+def text_names(tc) -> list[tuple[str, tuple[int, ...]]]:
+    """OpenAI state-dict names/shapes of the text tower (CLIP [3p]: token_embedding,
+    positional_embedding, transformer.resblocks.i.*, ln_final, text_projection)."""
+    D = tc.width
+    out = [("token_embedding.weight", (tc.vocab, D)), ("positional_embedding", (tc.context, D))]
+    for i in range(tc.layers):
+        r = f"transformer.resblocks.{i}."
+        out += [(r + "ln_1.weight", (D,)), (r + "ln_1.bias", (D,)),
+                (r + "attn.in_proj_weight", (3 * D, D)), (r + "attn.in_proj_bias", (3 * D,)),
+                (r + "attn.out_proj.weight", (D, D)), (r + "attn.out_proj.bias", (D,)),
+                (r + "ln_2.weight", (D,)), (r + "ln_2.bias", (D,)),
+                (r + "mlp.c_fc.weight", (4 * D, D)), (r + "mlp.c_fc.bias", (4 * D,)),
+                (r + "mlp.c_proj.weight", (D, 4 * D)), (r + "mlp.c_proj.bias", (D,))]
+    out += [("ln_final.weight", (D,)), ("ln_final.bias", (D,)),
+            ("text_projection", (D, tc.embed_dim))]
+    return out
+
+
+def synthetic_text_state_dict(tc, seed: int = 1) -> dict[str, torch.Tensor]:
+    """Seeded text-tower weights in the scales of CLIP.initialize_parameters [3p]
+    (token 0.02, positional 0.01, projection width^-0.5), LayerNorm/bias terms perturbed
+    like synthetic_state_dict so parity exercises every affine term."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for name, shape in text_names(tc):
+        if name == "positional_embedding":
+            t = torch.randn(shape, generator=g) * 0.01
+        elif name == "text_projection":
+            t = torch.randn(shape, generator=g) * tc.width ** -0.5
+        elif "ln_" in name:
+            t = torch.randn(shape, generator=g) * (0.1 if name.endswith("weight") else 0.02)
+            if name.endswith("weight"):
+                t += 1.0
+        else:
+            t = torch.randn(shape, generator=g) * 0.02
+        sd[name] = t.float().contiguous()
+    return sd
+
+
 def state_dict_checksum(sd: dict[str, torch.Tensor]) -> float:
     """Order-independent float64 checksum used to prove fixtures were regenerated identically."""
     return float(sum(float(v.double().abs().sum()) for v in sd.values()))

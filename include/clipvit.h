@@ -137,6 +137,48 @@ const char* clipvit_last_error(void);
 /* ABI version compiled into the library (CLIPVIT_ABI_VERSION). */
 int clipvit_abi_version(void);
 
+/* ---- Text tower ----
+ * Replaces model.encode_text(clip.tokenize(prompts)) [3p] as run once per prompt set by
+ * InteriorImageDetector (main.py:179-182) and CachedInteriorAnalyzer.
+ * _precompute_text_features_optimized (main.py:296-311); its normalised output is the T that
+ * clipvit_set_text_features takes. Geometry mirrors CLIP(transformer_width, _layers, _heads,
+ * context_length, vocab_size, embed_dim) [3p]. */
+typedef struct {
+    int width;          /* 512 (B models) / 768 (L/14), multiple of 256 */
+    int layers;         /* 12                                          */
+    int heads;          /* width / 64                                  */
+    int context;        /* 77                                          */
+    int vocab;          /* 49408 for the OpenAI BPE vocabulary          */
+    int embed_dim;      /* 512 / 768 (multiple of 64)                   */
+    int compute_dtype;  /* CLIPVIT_BF16 or CLIPVIT_F16                  */
+    int max_batch;      /* prompts per encode call                     */
+} clipvit_text_config;
+
+typedef struct clipvit_text_handle clipvit_text_handle;
+
+/* Text-tower model construction (the text half of clip.load, main.py:152 / main.py:241). */
+int clipvit_text_create(const clipvit_text_config* cfg, int device, clipvit_text_handle** out);
+
+/* Host fp32 tensors keyed by OpenAI names: token_embedding.weight [vocab, W],
+ * positional_embedding [context, W], transformer.resblocks.{i}.* (same leaves as the vision
+ * blocks), ln_final.{weight,bias}, text_projection [W, E]. visual.* names are ignored. */
+int clipvit_text_load_weights(clipvit_text_handle* h, const clipvit_tensor* tensors, size_t n);
+
+/* Replaces the text half of replace_linears_with_lora + load_lora_weights_to_model
+ * (main.py:62-113, main.py:247-251): targets "transformer.resblocks.{i}.mlp.c_fc.weight" etc.
+ * (where the shipped comprehensive_lora*.pth adapters bind). Same merge rule and reset
+ * semantics as clipvit_load_lora. */
+int clipvit_text_load_lora(clipvit_text_handle* h, const clipvit_lora* items, size_t n);
+
+/* Replaces model.encode_text(tokens) (main.py:181, main.py:308), optionally followed by the
+ * L2 normalisation of main.py:182 / main.py:309. tokens_dev: [B, context] int32 ids as
+ * clip.tokenize produces (sot ... eot, zero padded; pooled at the argmax id = eot);
+ * out_dev: [B, embed_dim] fp32. Ids outside [0, vocab) are clamped. */
+int clipvit_encode_text(clipvit_text_handle* h, void* stream, const int32_t* tokens_dev, int B,
+                        int l2_normalize, float* out_dev);
+
+int clipvit_text_destroy(clipvit_text_handle* h);
+
 /* ---- GPU preprocessing ----
  * Replaces preprocess(img) = clip's _transform(n_px) [3p] at main.py:201, main.py:438,
  * main.py:489 for images already decoded to RGB (load_image, main.py:119-128):

@@ -79,8 +79,10 @@ def quick_gelu(x: torch.Tensor) -> torch.Tensor:
     return x * torch.sigmoid(1.702 * x)
 
 
-def attention(x: torch.Tensor, in_w, in_b, out_w, out_b, heads: int) -> torch.Tensor:
-    """nn.MultiheadAttention(x, x, x, need_weights=False) restated for batch-first x [B,N,D]."""
+def attention(x: torch.Tensor, in_w, in_b, out_w, out_b, heads: int, mask=None) -> torch.Tensor:
+    """nn.MultiheadAttention(x, x, x, need_weights=False, attn_mask=mask) restated for
+    batch-first x [B,N,D] (mask: additive [N,N], CLIP's text tower passes -inf above the
+    diagonal)."""
     B, N, D = x.shape
     dh = D // heads
     qkv = x @ in_w.t() + in_b
@@ -89,6 +91,8 @@ def attention(x: torch.Tensor, in_w, in_b, out_w, out_b, heads: int) -> torch.Te
     k = k.reshape(B, N, heads, dh).transpose(1, 2)
     v = v.reshape(B, N, heads, dh).transpose(1, 2)
     s = (q @ k.transpose(-1, -2)) / math.sqrt(dh)
+    if mask is not None:
+        s = s + mask
     o = s.softmax(dim=-1) @ v
     o = o.transpose(1, 2).reshape(B, N, D)
     return o @ out_w.t() + out_b
@@ -116,6 +120,32 @@ def encode_image(sd: dict, geo: Geometry, pixels: torch.Tensor) -> torch.Tensor:
         x = x + (h @ sd[r + "mlp.c_proj.weight"].float().t() + sd[r + "mlp.c_proj.bias"].float())
     x = layer_norm(x[:, 0, :], sd[p + "ln_post.weight"], sd[p + "ln_post.bias"])
     return x @ sd[p + "proj"].float()
+
+
+def encode_text(sd: dict, tokens, heads: int = 8) -> torch.Tensor:
+    """``model.encode_text(tokens)`` [3p] (CLIP.encode_text; main.py:181, main.py:308) in fp32:
+
+        x = token_embedding[tokens] + positional_embedding
+        for each block (causal mask = -inf above the diagonal, CLIP.build_attention_mask):
+            x = x + attn(ln_1(x), mask); x = x + mlp(ln_2(x))
+        f = ln_final(x)[arange(B), tokens.argmax(-1)] @ text_projection
+    -> [B, embed_dim], not normalised (main.py:182 / main.py:309 normalise)."""
+    ids = torch.as_tensor(np.asarray(tokens)).long()
+    x = sd["token_embedding.weight"].float()[ids] + sd["positional_embedding"].float()[: ids.shape[1]]
+    n = ids.shape[1]
+    mask = torch.full((n, n), float("-inf")).triu_(1)
+    layers = sum(1 for k in sd if k.startswith("transformer.resblocks.") and k.endswith(".ln_1.weight"))
+    for i in range(layers):
+        r = f"transformer.resblocks.{i}."
+        h = layer_norm(x, sd[r + "ln_1.weight"], sd[r + "ln_1.bias"])
+        x = x + attention(h, sd[r + "attn.in_proj_weight"].float(), sd[r + "attn.in_proj_bias"].float(),
+                          sd[r + "attn.out_proj.weight"].float(), sd[r + "attn.out_proj.bias"].float(),
+                          heads, mask)
+        h = layer_norm(x, sd[r + "ln_2.weight"], sd[r + "ln_2.bias"])
+        h = quick_gelu(h @ sd[r + "mlp.c_fc.weight"].float().t() + sd[r + "mlp.c_fc.bias"].float())
+        x = x + (h @ sd[r + "mlp.c_proj.weight"].float().t() + sd[r + "mlp.c_proj.bias"].float())
+    x = layer_norm(x, sd["ln_final.weight"], sd["ln_final.bias"])
+    return x[torch.arange(x.shape[0]), ids.argmax(dim=-1)] @ sd["text_projection"].float()
 
 
 def merge_lora(W: torch.Tensor, A: torch.Tensor, B: torch.Tensor, scaling: float) -> torch.Tensor:
