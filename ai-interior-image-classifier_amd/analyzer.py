@@ -52,7 +52,9 @@ class InteriorAnalyzer:
                  dataset_json: str | Path = "interior_dataset.json",
                  text_features: dict[str, np.ndarray] | np.ndarray | None = None,
                  categories: dict[str, list[str]] | None = None, max_batch: int = 64,
-                 weights_seed: int = 0, gpu_preprocess: bool = True):
+                 weights_seed: int = 0, gpu_preprocess: bool = True,
+                 text_state_dict: dict | None = None, bpe_path: str | None = None, tokenizer=None,
+                 extra_segments: dict[str, tuple[list[str], list[str]]] | None = None):
         self.gpu_preprocess = bool(gpu_preprocess)  # _transform on the GPU (bit-identical)
         self.cfg = model if isinstance(model, ViTConfig) else get_config(model)
         self.engine = VisionEngine(self.cfg, device=device, compute_dtype=compute_dtype,
@@ -61,6 +63,7 @@ class InteriorAnalyzer:
                                     else synthetic_state_dict(self.cfg, weights_seed))
         self.use_lora = bool(use_lora)
         self.lora_report = None
+        ckpt = None
         if use_lora and lora_weights_path and Path(lora_weights_path).exists():
             ckpt = load_lora_checkpoint(lora_weights_path)
             items, loaded, missing = vision_adapters_from_checkpoint(ckpt, self.cfg, lora_rank, lora_alpha)
@@ -70,8 +73,41 @@ class InteriorAnalyzer:
             categories = L.extract_categories(L.load_training_data(dataset_json))
         self.all_categories = categories
         self.table = L.build_label_table(categories)
+        for name, (labels, texts) in (extra_segments or {}).items():  # e.g. worker.WORKER_STYLES
+            if len(labels) != len(texts) or not labels:
+                raise ValueError(f"extra segment {name!r}: labels and prompts must be non-empty, same length")
+            self.table.segments.append(name)
+            self.table.labels.append(list(labels))
+            self.table.texts.append(list(texts))
+        if text_features is None and text_state_dict is not None:
+            text_features = self._encode_labels(text_state_dict, ckpt, lora_rank, lora_alpha,
+                                                bpe_path, tokenizer, compute_dtype, device)
         T = self._text_matrix(text_features)
+        self.text_matrix = T  # [C, E] host copy of the label features the head uses
         self.engine.set_text_features(T, self.table.offsets)
+
+    def _encode_labels(self, text_sd, ckpt, rank, alpha, bpe_path, tokenizer, compute_dtype, device):
+        """The reference's two text caches on the GPU text tower: the detector prompts through
+        the BASE text tower (InteriorImageDetector's own clip.load, main.py:152/179-182), the
+        analyzer prompts through the LoRA text tower (main.py:241-251, 296-311)."""
+        from .config import text_config_for
+        from .lora import text_adapters_from_checkpoint
+        from .text import TextEngine
+        from .tokenizer import SimpleTokenizer
+        tok = tokenizer if tokenizer is not None else SimpleTokenizer(bpe_path=bpe_path)
+        tc = text_config_for(self.cfg, int(np.asarray(text_sd["token_embedding.weight"]).shape[0]))
+        te = TextEngine(tc, device, "bf16" if compute_dtype == "bf16" else "fp16", max_batch=256)
+        try:
+            te.load_state_dict(text_sd)
+            det = te.label_matrix(tok, self.table.texts[0])
+            if ckpt is not None:
+                items, loaded, _ = text_adapters_from_checkpoint(ckpt, tc.layers, rank, alpha, self.cfg.layers)
+                te.load_lora(items)
+                self.lora_report = dict(self.lora_report or {}, text_adapters=len(items))
+            rest = te.label_matrix(tok, [t for ts in self.table.texts[1:] for t in ts])
+        finally:
+            te.close()
+        return np.concatenate([det, rest], axis=0)
 
     def _text_matrix(self, text_features) -> np.ndarray:
         E = self.cfg.embed_dim

@@ -103,8 +103,9 @@ def state_dict_checksum(sd: dict[str, torch.Tensor]) -> float:
     return float(sum(float(v.double().abs().sum()) for v in sd.values()))
 
 
-def load_openai_checkpoint(path: str | Path) -> dict[str, torch.Tensor]:
-    """Local OpenAI CLIP checkpoint -> fp32 ``visual.*`` state dict.
+def load_openai_checkpoint(path: str | Path, text: bool = False) -> dict[str, torch.Tensor]:
+    """Local OpenAI CLIP checkpoint -> fp32 ``visual.*`` state dict (``text=True``: the text
+    tower's tensors instead, for TextEngine / InteriorAnalyzer(text_state_dict=...)).
 
     Tries a plain state dict with ``torch.load(weights_only=True)`` first; an OpenAI
     TorchScript archive (what clip.load downloads) is opened with ``torch.jit.load``, which
@@ -117,7 +118,10 @@ def load_openai_checkpoint(path: str | Path) -> dict[str, torch.Tensor]:
             sd = sd.state_dict()
     except Exception:
         sd = torch.jit.load(str(path), map_location="cpu").state_dict()
-    return {k: v.float().contiguous() for k, v in sd.items() if k.startswith("visual.")}
+    keep = (lambda k: not k.startswith("visual.") and k not in ("logit_scale", "input_resolution",
+                                                                 "context_length", "vocab_size")) \
+        if text else (lambda k: k.startswith("visual."))
+    return {k: v.float().contiguous() for k, v in sd.items() if keep(k)}
 
 
 def as_host_f32(t) -> np.ndarray:

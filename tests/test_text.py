@@ -168,3 +168,42 @@ def test_gpu_text_batch_tails_and_errors(gpu, tok):
     with pytest.raises(_lib.ClipVitError):
         eng.encode_text(np.zeros((9, 77), np.int32))  # above max_batch
     eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_analyzer_label_matrix_from_text_tower(gpu, tok, golden_dir, tmp_path):
+    """InteriorAnalyzer(text_state_dict=..., use_lora=True, lora_weights_path=ckpt): detector
+    rows through the base text tower, analyzer rows through the LoRA text tower (main.py:179-182
+    vs main.py:296-311), checkpoint in the shipped format (clip_model.transformer... keys)."""
+    from collections import OrderedDict
+    from interior_amd.analyzer import InteriorAnalyzer
+    from interior_amd.lora import load_lora_checkpoint, text_adapters_from_checkpoint
+    tc = _tc(tok)
+    sd = synthetic_text_state_dict(tc, 4)
+    g = torch.Generator().manual_seed(5)
+    ck = OrderedDict()
+    for i in range(12):
+        for leaf, (i_f, o_f) in (("c_fc", (512, 2048)), ("c_proj", (2048, 512))):
+            k = f"clip_model.transformer.resblocks.{i}.mlp.{leaf}.lora."
+            ck[k + "lora_A"] = torch.randn(i_f, 4, generator=g) * 0.02
+            ck[k + "lora_B"] = torch.randn(4, o_f, generator=g) * 0.02
+    path = tmp_path / "comprehensive_lora.pth"
+    torch.save(ck, path)
+    an = InteriorAnalyzer("ViT-B/32", use_lora=True, lora_weights_path=str(path), lora_rank=4,
+                          lora_alpha=8, device=gpu, compute_dtype="fp16",
+                          dataset_json=golden_dir / "interior_dataset.json", max_batch=4,
+                          text_state_dict=sd, tokenizer=tok)
+    assert an.lora_report["text_adapters"] == 24
+    texts = an.table.texts
+    det_ids = tok.tokenize(texts[0])
+    rest_ids = tok.tokenize([t for ts in texts[1:] for t in ts])
+    ref_det = torch.nn.functional.normalize(clip_ref.encode_text(sd, det_ids), dim=-1)
+    msd = dict(sd)
+    items, _, _ = text_adapters_from_checkpoint(load_lora_checkpoint(path), 12, 4, 8)
+    for a in items:
+        msd[a.target] = clip_ref.merge_lora(sd[a.target], torch.from_numpy(a.A), torch.from_numpy(a.B), a.scaling)
+    ref_rest = torch.nn.functional.normalize(clip_ref.encode_text(msd, rest_ids), dim=-1)
+    ref = torch.cat([ref_det, ref_rest]).numpy()
+    got = an.text_matrix
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() < 2e-3
