@@ -91,7 +91,8 @@ struct Workspace {
     bool used = false;
 };
 
-enum Fam { F_EMBED = 0, F_QKV, F_ATTN, F_OUT, F_LN, F_FC, F_PROJ, F_HEAD, F_COUNT };
+// F_TAIL: the last block's row-wise part on class-token rows (cls_tail)
+enum Fam { F_EMBED = 0, F_QKV, F_ATTN, F_OUT, F_LN, F_FC, F_PROJ, F_HEAD, F_TAIL, F_COUNT };
 
 struct Prof {
     std::vector<hipEvent_t> ev;
@@ -132,7 +133,7 @@ struct clipvit_handle {
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from in-model sweeps on MI355X
     // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
     // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles)
-    int var[5] = {8, 22, 13, 22, 22};
+    int var[5] = {80, 82, 13, 82, 22};
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
     int xcd[5] = {2, 2, 2, 2, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
@@ -150,6 +151,10 @@ struct clipvit_handle {
     // the following LayerNorm kernel does x += y (fp16 default; CLIPVIT_RESID16=0/1 overrides);
     // false = fp32 read-modify-write of x in the GEMM epilogue
     bool resid16 = false;
+    // deferred residual store (fp16 path, see forward()); CLIPVIT_DEFER_X=0 disables
+    bool defer_x = true;
+    // last block on class-token rows only (see cls_tail); CLIPVIT_CLS_PRUNE=0 disables
+    bool cls_prune = true;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -298,6 +303,53 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     return 0;
 }
 
+// Last block after its attention, on the class-token rows only (cls_prune): out_proj,
+// LayerNorm, MLP and the residual adds are row-wise, and ln_post(x[:, 0, :]) @ proj reads only
+// the class token, so the other B*(N-1) rows of this block are dead values. The CLS rows of x
+// and of the attention output are gathered into compact [B, D] buffers carved from u (dead
+// here); the arithmetic per row is the same kernels' (bit-identical result, tests/
+// test_gpu_parity.py::test_cls_prune_is_bit_identical).
+static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof) {
+    const int D = h->D, N = h->N;
+    const LayerW& ly = h->layers[h->cfg.layers - 1];
+    unsigned char* base = (unsigned char*)w->u;
+    float* xc = (float*)base;
+    u16* hc = (u16*)(base + (size_t)B * D * 4);
+    u16* yc = hc + (size_t)B * D;
+    u16* uc = yc + (size_t)B * D;
+    int rc;
+    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D);
+    auto g0 = [&](int epi, const void* A, const void* W, const float* bias, void* C, int n, int k) {
+        GemmArgs a{};
+        a.A = A; a.W = W; a.bias = bias; a.C = C;
+        a.M = B; a.N = n; a.K = k; a.ldc = n;
+        // 64x64 tiles (variant 4): the most workgroups for M = B rows (measured fastest on
+        // all three tail shapes, tools/tail_tune.py)
+        if (launch_gemm(s, h->dt, epi, a, 4) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
+            g_err = "cls tail gemm: unsupported shape";
+            return CLIPVIT_E_INVALID;
+        }
+        return 0;
+    };
+    if (h->resid16) {
+        if ((rc = g0(EPI_STORE, hc, ly.wout, ly.bout, yc, D, D))) return rc;
+        if (prof) prof->mark(s, F_TAIL);
+        launch_add_layernorm(s, h->dt, xc, yc, hc, ly.ln2g, ly.ln2b, B, D);
+    } else {
+        if ((rc = g0(EPI_RESID, hc, ly.wout, ly.bout, xc, D, D))) return rc;
+        if (prof) prof->mark(s, F_TAIL);
+        launch_layernorm(s, h->dt, xc, hc, ly.ln2g, ly.ln2b, B, D);
+    }
+    if (prof) prof->mark(s, F_TAIL);
+    if ((rc = g0(EPI_GELU, hc, ly.wfc, ly.bfc, uc, 4 * D, D))) return rc;
+    if (prof) prof->mark(s, F_TAIL);
+    if ((rc = g0(EPI_RESID, uc, ly.wproj, ly.bproj, xc, D, 4 * D))) return rc;
+    if (prof) prof->mark(s, F_TAIL);
+    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E);
+    if (prof) prof->mark(s, F_HEAD);
+    return 0;
+}
+
 // MX-fp8 encoder forward (same sequence as forward()). Blocks listed in
 // mx8_skip run the 16-bit path; every LayerNorm writes the format its consumer block uses.
 static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
@@ -374,20 +426,31 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                     B, N, D);
     if (prof) prof->mark(s, F_EMBED);
     // 16-bit residual branch outputs (resid16) reuse the qkv buffer: qkv is dead once attention
-    // has read it, and the branch output of c_proj is consumed before the next QKV GEMM
+    // has read it. y = out_proj's branch, y2 = c_proj's. With deferred adds (defer_x), the add
+    // after out_proj only feeds ln_2 (x is not written back) and the add after c_proj computes
+    // (x + y) + y2 — the same fp32 additions in the same order — and stores x once per block.
     void* y = w->qkv;
-    for (int i = 0; i < h->cfg.layers; ++i) {
+    void* y2 = (u16*)w->qkv + (size_t)M * D;
+    const int nl = h->cfg.layers;
+    for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
-        const bool last = i + 1 == h->cfg.layers;
+        const bool last = i + 1 == nl;
         if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (prof) prof->mark(s, F_ATTN);
+        if (last && h->cls_prune) {
+            if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
+            HIPCHK(hipGetLastError());
+            return 0;
+        }
+        const bool defer = h->resid16 && h->defer_x && !last;
         if (h->resid16) {
             if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT))) return rc;
             if (prof) prof->mark(s, F_OUT);
-            launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D);
+            else launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
         } else {
             if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT))) return rc;
             if (prof) prof->mark(s, F_OUT);
@@ -398,9 +461,12 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             return rc;
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
-            if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, y, M, D, 4 * D, D, R_PROJ))) return rc;
+            void* yo = defer ? y2 : y;
+            if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, yo, M, D, 4 * D, D, R_PROJ))) return rc;
             if (prof) prof->mark(s, F_PROJ);
-            launch_add_layernorm(s, h->dt, w->x, y, w->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+            const LayerW& nx = h->layers[i + 1];
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D);
+            else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
             if ((rc = gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)))
@@ -525,6 +591,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->dt = h->mx8 ? CLIPVIT_BF16 : c.compute_dtype;  // 16-bit type of everything not MX-fp8
     h->resid16 = !h->mx8 && h->dt == CLIPVIT_F16;
     if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;
@@ -875,9 +943,9 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
-    // 16-bit-output kernels (variants 30-39, or epi 10 / 11 = 16-bit STORE / GELU on any
-    // variant): run, then widen to fp32
-    if ((variant >= 30 && variant < 40) || epi >= 10) {
+    // 16-bit-output kernels (variants 30-39 and 80-89, or epi 10 / 11 = 16-bit STORE / GELU on
+    // any variant): run, then widen to fp32
+    if ((variant >= 30 && variant < 40) || (variant >= 80 && variant < 90) || epi >= 10) {
         if (epi >= 10) epi -= 10;
         if (epi == 2) {
             hipFreeAsync(Wp, s);

@@ -242,6 +242,11 @@ void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, u
                             int N, int K, int Kp);
 void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
                           const float* b, int rows, int D);
+// x' = x + y (+ y2); h = LayerNorm(x'). y2 == nullptr: x' is NOT stored (deferred: the next
+// call adds both branch outputs in the same order); y2 != nullptr: x' is stored.
+void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
+                                   void* h, const float* g, const float* b, int rows, int D);
+void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D);
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
                          const float* g, const float* b, int rows, int D);
 void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,

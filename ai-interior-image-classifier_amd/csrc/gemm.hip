@@ -338,6 +338,58 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 
     // ---- epilogue (same contract as gemm_nt_kernel) ----
     const int g = lg;
+    if constexpr (SM == 3 && (EPI == EPI_STORE || EPI == EPI_GELU)) {
+        // Row-contiguous stores staged through LDS: the accumulator layout gives each lane 32 B
+        // of one row, so direct stores cover 16 rows x 4 scattered 16-B pieces per
+        // wave-instruction; here the tile is first written to LDS (row-major, 16-B chunk
+        // c ^ (row & 7): conflict-free ds_write_b128), then every wave-instruction stores whole
+        // rows (64 lanes x 16 B contiguous).
+        constexpr int ROWB = BN * 2, CPR = ROWB / 16;
+        static_assert(BM * ROWB <= NS * STAGE, "epilogue tile must fit in the LDS ring");
+        __builtin_amdgcn_s_barrier();  // every wave is done reading the ring
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int r = wm * TM + fm * 16 + lrow;
+#pragma unroll
+            for (int q = 0; q < FN / 4; ++q) {
+                const int nl = wn * TN + q * 64 + 16 * g;
+                float v[16];
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[4 * q + f][fm][rr];
+                if (a.bias) {
+                    const float4* b4 = (const float4*)(a.bias + n0 + nl);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float4 bb = b4[i];
+                        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+                    }
+                }
+                if constexpr (EPI == EPI_GELU) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                }
+                const int c0 = nl >> 3;  // 16-B chunk of the row
+                unsigned char* rowp = smem + r * ROWB;
+                *(uint4*)(rowp + (((c0) ^ (r & 7)) << 4)) =
+                    make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+                *(uint4*)(rowp + (((c0 + 1) ^ (r & 7)) << 4)) =
+                    make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        unsigned char* Cb = (unsigned char*)a.C;
+#pragma unroll 4
+        for (int i = tid; i < BM * CPR; i += NT) {
+            const int r = i / CPR, c = i % CPR;
+            const int m = m0 + r;
+            const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
+            if (m < a.M) *(uint4*)(Cb + ((size_t)m * a.ldc + n0) * 2 + c * 16) = val;
+        }
+        return;
+    }
     OutStore<SM> out(a.C);
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
@@ -1237,6 +1289,19 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             launch_pipe<T, 160, 256, 2, 4, 2, 1>(s, epi, a);
             return 0;
         // ---- write-through (sc1) output stores: 50 = 8, 51 = 21, 52 = 13, 53 = 14 ----
+        // ---- LDS-staged row-contiguous 16-bit epilogue (SM = 3) of 8 / 13 / 22 ----
+        case 80:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 256, 256, 2, 4, 2, 3>(s, epi, a);
+            return 0;
+        case 81:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 128, 128, 4, 2, 2, 3>(s, epi, a);
+            return 0;
+        case 82:
+            if (a.N % 128) return -1;
+            launch_pipe<T, 160, 128, 2, 2, 2, 3>(s, epi, a);
+            return 0;
         case 50:
             if (a.N % 256) return -1;
             launch_pipe<T, 256, 256, 2, 4, 2, 2>(s, epi, a);

@@ -167,8 +167,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // x[row] += y[row] (16-bit branch output of out_proj / c_proj); h[row] = LayerNorm(x[row]).
 // Moves the residual add out of the GEMM epilogue (which then only stores y): the GEMM no
 // longer reads x, and this kernel streams x, y -> x, h in one pass.
-template <typename T, int V>
+template <typename T, int V, bool STORE_X = true, bool TWO = false>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, const u16* __restrict__ y,
+                                                            const u16* __restrict__ y2,
                                                             u16* __restrict__ h, const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
     const int lane = threadIdx.x & 63;
@@ -178,19 +179,27 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
     float* xr = x + (size_t)row * D;
     const u16* yr = y + (size_t)row * D;
     float4 v[V];
-    uint2 w[V];
+    uint2 w[V], w2[V];
 #pragma unroll
     for (int i = 0; i < V; ++i) {
         v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
         w[i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
+        if constexpr (TWO) w2[i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
     }
 #pragma unroll
     for (int i = 0; i < V; ++i) {
+        // (x + y) + y2: the same fp32 additions, in the same order, as two separate residual adds
         v[i].x += T::to_f32((u16)(w[i].x & 0xffff));
         v[i].y += T::to_f32((u16)(w[i].x >> 16));
         v[i].z += T::to_f32((u16)(w[i].y & 0xffff));
         v[i].w += T::to_f32((u16)(w[i].y >> 16));
-        *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+        if constexpr (TWO) {
+            v[i].x += T::to_f32((u16)(w2[i].x & 0xffff));
+            v[i].y += T::to_f32((u16)(w2[i].x >> 16));
+            v[i].z += T::to_f32((u16)(w2[i].y & 0xffff));
+            v[i].w += T::to_f32((u16)(w2[i].y >> 16));
+        }
+        if constexpr (STORE_X) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
     }
     ln_row<V>(v, gm, bt, lane, (float)D);
     store_row16<T, V>(h + (size_t)row * D, v, lane);
@@ -235,10 +244,47 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
                           const float* b, int rows, int D) {
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
-        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, (u16*)h, g, b, rows));
+        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
     } else {
-        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, (u16*)h, g, b, rows));
+        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
     }
+}
+
+template <typename T, int V>
+static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2, u16* h, const float* g,
+                            const float* b, int rows) {
+    dim3 grid((rows + 3) / 4), block(256);
+    if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
+    else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
+}
+
+void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
+                                   void* h, const float* g, const float* b, int rows, int D) {
+    if (dtype == 2) {
+        DISPATCH_V(D, add_ln_deferred<F16, V>(s, x, (const u16*)y, (const u16*)y2, (u16*)h, g, b, rows));
+    } else {
+        DISPATCH_V(D, add_ln_deferred<BF16, V>(s, x, (const u16*)y, (const u16*)y2, (u16*)h, g, b, rows));
+    }
+}
+
+// CLS rows of a [B*N, D] token buffer pair -> compact [B, D] buffers (x fp32, h 16-bit):
+// the last block's row-wise ops (out_proj, LayerNorm, MLP) only matter for the class token,
+// which is all that ln_post(x[:, 0, :]) @ proj reads.
+__global__ __launch_bounds__(256) void gather_cls_kernel(const float* __restrict__ x, const u16* __restrict__ h,
+                                                         float* __restrict__ xc, u16* __restrict__ hc, int N,
+                                                         int D, int B) {
+    const int b = blockIdx.x;
+    if (b >= B) return;
+    const float* xs = x + (size_t)b * N * D;
+    const u16* hs = h + (size_t)b * N * D;
+    for (int c = threadIdx.x * 4; c < D; c += 1024) {
+        *(float4*)(xc + (size_t)b * D + c) = *(const float4*)(xs + c);
+        *(uint2*)(hc + (size_t)b * D + c) = *(const uint2*)(hs + c);
+    }
+}
+
+void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D) {
+    gather_cls_kernel<<<B, 256, 0, s>>>(x, (const u16*)h, xc, (u16*)hc, N, D, B);
 }
 
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,

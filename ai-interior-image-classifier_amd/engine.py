@@ -175,12 +175,12 @@ class VisionEngine:
     def profile_forward(self, pixels: torch.Tensor, iters: int = 5) -> dict[str, float]:
         """Per-kernel-family device milliseconds of one forward (HIP events between stages)."""
         pixels = self._pixels(pixels)
-        ms = (ctypes.c_float * 9)()
+        ms = (ctypes.c_float * 10)()
         with torch.cuda.device(self.device):
             _lib.check(self._L.clipvit_profile_forward(self._h, self._stream(), _vp(pixels),
                                                        _PIX_DT[pixels.dtype], pixels.shape[0], iters, ms))
         keys = ("patch_embed", "qkv_gemm", "attention", "out_proj_gemm", "layernorm", "fc_gemm",
-                "proj_gemm", "head", "lane_batch")
+                "proj_gemm", "head", "cls_tail", "lane_batch")
         return {k: float(v) for k, v in zip(keys, ms)}
 
 

@@ -158,10 +158,15 @@ def main():
     lane_b = int(fam.pop("lane_batch"))  # images per launch (per stream lane)
     D, N, M = cfg.width, cfg.tokens, lane_b * cfg.tokens
     mlp_flop = 2.0 * M * D * 4 * D  # c_fc and c_proj each
-    mlp_ms = (fam["fc_gemm"] + fam["proj_gemm"]) / (2 * cfg.layers)  # per launch
+    full_layers = cfg.layers - (1 if fam.get("cls_tail", 0.0) > 0 else 0)  # full-M MLP launches
+    mlp_ms = (fam["fc_gemm"] + fam["proj_gemm"]) / (2 * full_layers)  # per launch
     achieved = mlp_flop / (mlp_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[a.dtype]
-    model_tflops = value / world * cfg.gflop_per_image() / 1e3
+    # FLOPs executed per image: the last block's out_proj/MLP run on the class token only
+    # (dead-row elimination, DESIGN.md §Last block), so those N-1 rows are not counted
+    pruned = 2.0 * (N - 1) * D * 9 * D / 1e9 if fam.get("cls_tail", 0.0) > 0 else 0.0
+    gflop_img = cfg.gflop_per_image() - pruned
+    model_tflops = value / world * gflop_img / 1e3
 
     line = {
         "metric": "images/sec @ 224x224 bs=256, ViT-B/32+LoRA, 1/2/4/8 MI355X; % MFMA roofline",
@@ -184,6 +189,7 @@ def main():
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),
                      "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(mlp_ms, 5),
                      "model_mfma_frac": round(model_tflops / peak, 4),
+                     "gflop_per_image_executed": round(gflop_img, 4),
                      "family_ms_per_forward": {k: round(v, 4) for k, v in fam.items()}},
         "cpu_baseline": None,
     }

@@ -250,8 +250,9 @@ int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* o
 /* Time `iters` launches of ONE lane's encoder forward (the per-stream batch the call path
  * launches for B images: ceil(B/2) when the batch is split over the two lane streams, else B)
  * serialised on `stream`; returns the average per-kernel-family device time (ms) into
- * out_ms[0..7]: 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm,
- * 5 fc gemm, 6 proj gemm, 7 head (ln_post+proj); out_ms[8] = the lane batch profiled.
+ * out_ms[0..8]: 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm,
+ * 5 fc gemm, 6 proj gemm, 7 head (ln_post+proj), 8 the last block's row-wise part on
+ * class-token rows (0 when the full last block runs); out_ms[9] = the lane batch profiled.
  * Requires weights loaded. Used by bench.py's roofline probe. */
 int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype,
                             int B, int iters, float* out_ms);

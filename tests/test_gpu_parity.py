@@ -155,6 +155,30 @@ def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
     assert torch.equal(outs[0][2], outs[1][2])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp16", "bf16"])
+def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
+    """The last block on class-token rows only (CLIPVIT_CLS_PRUNE) and the deferred residual
+    store (CLIPVIT_DEFER_X) execute the same per-row fp32 operations in the same order, so the
+    features equal the full computation's bit for bit (B/32 and the N = 197 B/16 geometry)."""
+    for cfg, B in ((C.VIT_B32, 67), (C.VIT_B16, 9)):
+        sd = synthetic_state_dict(cfg, 0)
+        ad = synthetic_adapters(cfg, rank=8)
+        px = _pixels(B, cfg.image_size, seed=23).to(gpu)
+        outs = []
+        for prune, defer in (("0", "0"), ("1", "1"), ("1", "0"), ("0", "1")):
+            monkeypatch.setenv("CLIPVIT_CLS_PRUNE", prune)
+            monkeypatch.setenv("CLIPVIT_DEFER_X", defer)
+            eng = VisionEngine(cfg, 0, dtype, max_batch=B)
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+            eng.close()
+        for o in outs[1:]:
+            assert torch.equal(outs[0], o), (cfg.name, dtype)
+
+
 def test_concurrent_host_threads(gpu):
     """The reference calls encode_image from ThreadPoolExecutor(4) (main.py:345-346); the
     handle must give every thread its own workspace and correct results."""
