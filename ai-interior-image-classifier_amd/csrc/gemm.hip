@@ -1302,6 +1302,20 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 128) return -1;
             launch_pipe<T, 160, 128, 2, 2, 2, 3>(s, epi, a);
             return 0;
+        // 224-row tiles: M = 12800 -> 58 M-tiles, i.e. 696 tiles at N = 3072 (2.7 rounds of
+        // 256 CUs) with the fill bytes per FLOP of a 256-wide tile
+        case 83:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 224, 256, 2, 4, 2, 3>(s, epi, a);
+            return 0;
+        case 84:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 224, 256, 2, 4, 2>(s, epi, a);
+            return 0;
+        case 85:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 192, 256, 2, 4, 2, 3>(s, epi, a);
+            return 0;
         case 50:
             if (a.N % 256) return -1;
             launch_pipe<T, 256, 256, 2, 4, 2, 2>(s, epi, a);

@@ -36,6 +36,10 @@ def roles_for_trace(rows):
             out.append("patch_gemm"); pos = 0; continue
         if "embed_ln" in n:
             out.append("embed_ln"); pos = 0; continue
+        if "gather_cls" in n:  # last block on class-token rows (cls_tail)
+            out.append("cls_tail"); pos = "tail"; continue
+        if pos == "tail" and (gemm_like(n) or "layernorm" in n):
+            out.append("cls_tail"); continue
         if "cls_ln_proj" in n:
             out.append("head_proj"); pos = None; continue
         if "logits_kernel" in n:
