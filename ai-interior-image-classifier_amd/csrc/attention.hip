@@ -19,6 +19,8 @@
 // K in LDS: 128-B rows, 16-B chunk swizzle c ^ (row & 7) (conflict-free ds_read_b128).
 // V in LDS transposed (Vt[d][key]), 8-B chunk swizzle (key/4) ^ 2*((d>>1)&7): each
 // ds_read_b64 of a V^T fragment is conflict-free.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace clipvit {
@@ -165,6 +167,176 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// attention_v2_kernel (non-causal, the vision tower's default): same math and register
+// layout as attention_kernel, but K and V blocks reach LDS by global_load_lds (async, no VGPR
+// staging) into a 2-stage ring, so block kb+1 streams in while block kb is computed, and V is
+// stored row-major exactly like K (16-B chunk c ^ (key & 7)) and read TRANSPOSED by
+// ds_read_b64_tr_b16: lane group g, lane 4q + p supplies key r0 + q, columns 4p .. 4p + 3;
+// lane i receives column d = 16 dt + i of the 4 keys — the A operand of O^T += V^T P^T with
+// the k order of P (k-slot (g, e) <-> key 32 st + 16 (e >> 2) + 4 g + (e & 3)). No scalar
+// LDS transposes, no __syncthreads (raw s_barrier + counted vmcnt keep the next block's loads
+// in flight). Rows past the sequence are clamped in bounds and masked to -inf in S.
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T>
+__global__ __launch_bounds__(256) void attention_v2_kernel(const u16* __restrict__ qkv,
+                                                           u16* __restrict__ out, int N, int H) {
+    typedef typename T::vec8 vec8;
+    constexpr int STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+
+    const int D = H * 64;
+    const int ld = 3 * D;
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, g = lane >> 4;
+    const size_t base = (size_t)b * N;
+
+    const int q = qb * 64 + wave * 16 + j;
+    const int qc = min(q, N - 1);
+    const u16* qrow = qkv + (base + qc) * ld + h * 64;
+    vec8 qf[2];
+    qf[0] = *(const vec8*)(qrow + 8 * g);
+    qf[1] = *(const vec8*)(qrow + 32 + 8 * g);
+
+    // glds assignment: wave w fills key rows [16 w, 16 w + 16) of K and of V (2 x 1 KB each)
+    const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
+    auto issue = [&](int kb, int st) {
+        unsigned char* dst = smem + st * STAGE;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int row = wave * 16 + r * 8 + (lane >> 3);
+            const int key = min(kb * 64 + row, N - 1);
+            const int c = (lane & 7) ^ (row & 7);
+            const unsigned char* ks = src + (size_t)key * ld * 2 + c * 16;
+            glds16(ks, dst + (wave * 16 + r * 8) * 128);
+            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * 16 + r * 8) * 128);
+        }
+    };
+
+    f32x4 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+    const float scale = 0.125f;  // 1/sqrt(64)
+    const int nkb = (N + 63) >> 6;
+
+    issue(0, 0);
+    if (nkb > 1) issue(1, 1);
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int st = kb & 1;
+        if (kb + 1 < nkb) vm_wait<4>();  // block kb landed (this wave's part); kb+1 may fly
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();      // ... and every wave's part
+        const unsigned char* Ks = smem + st * STAGE;
+        const unsigned char* Vs = Ks + 8192;
+
+        f32x4 s[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int row = kt * 16 + j;
+#pragma unroll
+            for (int ds = 0; ds < 2; ++ds) {
+                const int c = ((ds << 2) | g) ^ (row & 7);
+                const vec8 kf = *(const vec8*)(Ks + row * 128 + (c << 4));
+                s[kt] = T::mfma16(kf, qf[ds], s[kt]);
+            }
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = kb * 64 + kt * 16 + 4 * g + r;
+                const float v = key < N ? s[kt][r] * scale : -INFINITY;
+                s[kt][r] = v;
+                mloc = fmaxf(mloc, v);
+            }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = __expf(m_run - m_new);
+        m_run = m_new;
+        float lsum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float p = __expf(s[kt][r] - m_new);
+                s[kt][r] = p;
+                lsum += p;
+            }
+        l_run = l_run * alpha + lsum;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] *= alpha;
+
+        // V^T fragments: all 16 transposed reads first (inline asm: a builtin tr-read makes
+        // hipcc drain vmcnt(0) before it, i.e. wait for the NEXT block's glds), then one
+        // lgkmcnt(0) + sched_barrier (hipcc would otherwise hoist the MFMAs past the wait)
+        const int tq = (lane & 15) >> 2, tp = lane & 3;  // lane 4q + p of its 16-lane group
+        const unsigned vbase = (unsigned)(size_t)(LDS_AS const unsigned char*)Vs;
+        u32x2 vr[2][4][2];
+#pragma unroll
+        for (int stp = 0; stp < 2; ++stp)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const int k = 32 * stp + 16 * hf + 4 * g + tq;  // this lane's key row
+                    const int cl = 2 * dt + (tp >> 1);               // logical chunk of d = 16 dt + 4 p
+                    const unsigned addr = vbase + k * 128 + ((cl ^ (k & 7)) << 4) + 8 * (tp & 1);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[stp][dt][hf]) : "v"(addr) : "memory");
+                }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int stp = 0; stp < 2; ++stp) {
+            vec8 pf;
+            {
+                unsigned w[4] = {pack2<T>(s[2 * stp][0], s[2 * stp][1]), pack2<T>(s[2 * stp][2], s[2 * stp][3]),
+                                 pack2<T>(s[2 * stp + 1][0], s[2 * stp + 1][1]),
+                                 pack2<T>(s[2 * stp + 1][2], s[2 * stp + 1][3])};
+                pf = __builtin_bit_cast(vec8, *(uint4*)w);
+            }
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const uint4 vv = make_uint4(vr[stp][dt][0].x, vr[stp][dt][0].y, vr[stp][dt][1].x, vr[stp][dt][1].y);
+                o[dt] = T::mfma16(__builtin_bit_cast(vec8, vv), pf, o[dt]);
+            }
+        }
+        if (kb + 2 < nkb) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the stage done
+            __builtin_amdgcn_s_barrier();        // ... every wave's
+            issue(kb + 2, st);
+        }
+    }
+
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+    if (q < N) {
+        const float inv = 1.0f / l_run;
+        u16* orow = out + (base + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            uint2 w;
+            w.x = pack2<T>(o[dt][0] * inv, o[dt][1] * inv);
+            w.y = pack2<T>(o[dt][2] * inv, o[dt][3] * inv);
+            *(uint2*)(orow + dt * 16 + 4 * g) = w;
+        }
+    }
+}
+
+static bool attn_v2() {
+    static const bool on = [] {
+        const char* v = getenv("CLIPVIT_ATTN_V2");
+        return !v || atoi(v) != 0;
+    }();
+    return on;
+}
+
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal) {
     dim3 grid((N + 63) / 64, H, B), block(256);
@@ -173,6 +345,11 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
             attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else
             attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v2()) {
+        if (dtype == 2)
+            attention_v2_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v2_kernel<BF16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else if (dtype == 2) {
         attention_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else {

@@ -385,6 +385,11 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
         if (prof) prof->mark(s, F_ATTN);
+        if (i + 1 == h->cfg.layers && h->cls_prune && !q) {  // bf16 last block: class-token rows only
+            if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
+            HIPCHK(hipGetLastError());
+            return 0;
+        }
         rc = q ? gemm8(s, h, EPI_RESID, q8, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT)
                : gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT);
         if (rc) return rc;

@@ -163,7 +163,8 @@ def _ref_attention(qkv, B, N, H):
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2), (torch.float16, 3e-3)])
-@pytest.mark.parametrize("B,N,H", [(3, 50, 12), (2, 197, 12), (1, 577, 16), (2, 1, 12), (1, 65, 12)])
+@pytest.mark.parametrize("B,N,H", [(3, 50, 12), (2, 197, 12), (1, 577, 16), (2, 1, 12), (1, 65, 12),
+                                   (2, 130, 12), (1, 300, 16)])
 def test_attention(gpu, dtype, tol, B, N, H):
     g = torch.Generator(device=gpu).manual_seed(B * N * H)
     qkv = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).to(dtype)
