@@ -179,9 +179,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
 // in flight). Rows past the sequence are clamped in bounds and masked to -inf in S.
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-template <typename T>
-__global__ __launch_bounds__(256) void attention_v2_kernel(const u16* __restrict__ qkv,
-                                                           u16* __restrict__ out, int N, int H) {
+// QW waves per workgroup = 16 QW queries; every wave loads 64 / QW key rows of K and of V
+// per block (QW = 8 halves the K/V re-reads of long sequences: the fill path bounds them).
+template <typename T, int QW = 4>
+__global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __restrict__ qkv,
+                                                               u16* __restrict__ out, int N, int H) {
     typedef typename T::vec8 vec8;
     constexpr int STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
@@ -194,25 +196,26 @@ __global__ __launch_bounds__(256) void attention_v2_kernel(const u16* __restrict
     const int j = lane & 15, g = lane >> 4;
     const size_t base = (size_t)b * N;
 
-    const int q = qb * 64 + wave * 16 + j;
+    const int q = qb * (16 * QW) + wave * 16 + j;
     const int qc = min(q, N - 1);
     const u16* qrow = qkv + (base + qc) * ld + h * 64;
     vec8 qf[2];
     qf[0] = *(const vec8*)(qrow + 8 * g);
     qf[1] = *(const vec8*)(qrow + 32 + 8 * g);
 
-    // glds assignment: wave w fills key rows [16 w, 16 w + 16) of K and of V (2 x 1 KB each)
+    // glds assignment: wave w fills key rows [RW w, RW w + RW) of K and of V (1 KB pieces)
+    constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
     const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
     auto issue = [&](int kb, int st) {
         unsigned char* dst = smem + st * STAGE;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int row = wave * 16 + r * 8 + (lane >> 3);
+        for (int r = 0; r < RW / 8; ++r) {
+            const int row = wave * RW + r * 8 + (lane >> 3);
             const int key = min(kb * 64 + row, N - 1);
             const int c = (lane & 7) ^ (row & 7);
             const unsigned char* ks = src + (size_t)key * ld * 2 + c * 16;
-            glds16(ks, dst + (wave * 16 + r * 8) * 128);
-            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * 16 + r * 8) * 128);
+            glds16(ks, dst + (wave * RW + r * 8) * 128);
+            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * RW + r * 8) * 128);
         }
     };
 
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(256) void attention_v2_kernel(const u16* __restrict
     if (nkb > 1) issue(1, 1);
     for (int kb = 0; kb < nkb; ++kb) {
         const int st = kb & 1;
-        if (kb + 1 < nkb) vm_wait<4>();  // block kb landed (this wave's part); kb+1 may fly
+        if (kb + 1 < nkb) vm_wait<LPB>();  // block kb landed (this wave's part); kb+1 may fly
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();      // ... and every wave's part
         const unsigned char* Ks = smem + st * STAGE;
@@ -345,6 +348,12 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
             attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else
             attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v2() && N > 128) {  // long sequences: 128 queries per workgroup
+        dim3 g8((N + 127) / 128, H, B);
+        if (dtype == 2)
+            attention_v2_kernel<F16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v2_kernel<BF16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else if (attn_v2()) {
         if (dtype == 2)
             attention_v2_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
