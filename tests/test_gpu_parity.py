@@ -179,6 +179,19 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
             assert torch.equal(outs[0], o), (cfg.name, dtype)
 
 
+@pytest.mark.parametrize("dtype,pdt", [("fp16", torch.float16), ("bf16", torch.bfloat16)])
+def test_pixel_dtype_16bit_input_is_bit_identical(gpu, dtype, pdt):
+    """im2col rounds fp32 pixels to the MFMA operand type; 16-bit pixels of that type (what
+    bench.py feeds, clip's image.type(model.dtype)) give bit-identical features."""
+    cfg = C.VIT_B32
+    eng, _ = _engine(cfg, dtype, lora_rank=8, max_batch=256)
+    px = _pixels(33, 224, seed=29).to(gpu)
+    a = eng.encode_image(px).clone()
+    b = eng.encode_image(px.to(pdt)).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 def test_concurrent_host_threads(gpu):
     """The reference calls encode_image from ThreadPoolExecutor(4) (main.py:345-346); the
     handle must give every thread its own workspace and correct results."""
