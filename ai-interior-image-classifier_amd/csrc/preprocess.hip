@@ -24,6 +24,7 @@
 // writing [B, 3, n_px, n_px] fp32 / bf16 / fp16 for clipvit_encode_image / clipvit_classify.
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -219,6 +220,21 @@ int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit
     std::vector<int32_t> plans;
     long long inter_bytes = 0;
     int maxR = 0;
+    // plans depend only on (source size, resized size): one copy per distinct axis pair (a
+    // batch of same-size photos uploads two plans, not 2 B)
+    struct PlanRef { int b, k, ks, first; };
+    std::map<std::pair<int, int>, PlanRef> cache;
+    auto plan_of = [&](int in, int out) -> PlanRef {
+        auto it = cache.find({in, out});
+        if (it != cache.end()) return it->second;
+        const Plan p = make_plan(in, out);
+        PlanRef r{(int)plans.size(), 0, p.ksize, p.bounds[0]};
+        plans.insert(plans.end(), p.bounds.begin(), p.bounds.end());
+        r.k = (int)plans.size();
+        plans.insert(plans.end(), p.kk.begin(), p.kk.end());
+        cache.emplace(std::make_pair(in, out), r);
+        return r;
+    };
     for (int b = 0; b < B; ++b) {
         const clipvit_image& im = images[b];
         if (im.width <= 0 || im.height <= 0 || im.offset < 0)
@@ -226,29 +242,25 @@ int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit
         int nw, nh;
         resize_size(im.width, im.height, n_px, nw, nh);
         if (nw < n_px || nh < n_px) PP_FAIL(CLIPVIT_E_INVALID, "resized image smaller than the crop");
-        const Plan ph = make_plan(im.width, nw), pv = make_plan(im.height, nh);
+        const PlanRef ph = plan_of(im.width, nw), pv = plan_of(im.height, nh);
         ImgDesc& d = descs[b];
         d.src = im.offset;
         d.W = im.width;
         d.H = im.height;
         d.left = crop_offset(nw, n_px);
         d.top = crop_offset(nh, n_px);
-        d.ksh = ph.ksize;
-        d.ksv = pv.ksize;
-        d.rlo = pv.bounds[2 * d.top];
+        d.ksh = ph.ks;
+        d.ksv = pv.ks;
+        d.rlo = plans[pv.b + 2 * d.top];
         const int last = d.top + n_px - 1;
-        d.R = pv.bounds[2 * last] + pv.bounds[2 * last + 1] - d.rlo;
+        d.R = plans[pv.b + 2 * last] + plans[pv.b + 2 * last + 1] - d.rlo;
         d.inter = inter_bytes;
         inter_bytes += (long long)d.R * n_px * 3;
         maxR = std::max(maxR, d.R);
-        d.bh = (int)plans.size();
-        plans.insert(plans.end(), ph.bounds.begin(), ph.bounds.end());
-        d.kh = (int)plans.size();
-        plans.insert(plans.end(), ph.kk.begin(), ph.kk.end());
-        d.bv = (int)plans.size();
-        plans.insert(plans.end(), pv.bounds.begin(), pv.bounds.end());
-        d.kv = (int)plans.size();
-        plans.insert(plans.end(), pv.kk.begin(), pv.kk.end());
+        d.bh = ph.b;
+        d.kh = ph.k;
+        d.bv = pv.b;
+        d.kv = pv.k;
     }
     // one device block: descs | plans | intermediate
     const size_t dbytes = descs.size() * sizeof(ImgDesc), pbytes = plans.size() * sizeof(int32_t);
