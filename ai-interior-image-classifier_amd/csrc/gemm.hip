@@ -190,7 +190,9 @@ __device__ __forceinline__ void wait_tile(int r) {
 
 // ABL (timing-only ablation builds, results wrong): bit0 no global->LDS loads, bit1 no LDS
 // fragment reads, bit2 no MFMAs.
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int ABL = 0>
+// PRIO: s_setprio(1) around each MFMA cluster (the arbiter then issues a wave's MFMAs ahead of
+// the other wave's LDS / global instructions on the same SIMD).
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int ABL = 0, int PRIO = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
@@ -298,17 +300,19 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
 
     auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
         if constexpr (ABL & 4) {
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm) asm volatile("" ::"v"(af[fm]));
 #pragma unroll
             for (int fn = 0; fn < FN; ++fn) asm volatile("" ::"v"(wf[fn]));
-            return;
+        } else {
+#pragma unroll
+            for (int fn = 0; fn < FN; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
         }
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-            for (int fm = 0; fm < FM; ++fm) acc[fn][fm] = T::mfma16(wf[fn], af[fm], acc[fn][fm]);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
     };
 
     vec8 a0[FM], w0[FN], a1[FM], w1[FN];
@@ -681,6 +685,19 @@ static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
         case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
         case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
         case EPI_DISCARD: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_DISCARD><<<grid, block, 0, s>>>(a); break;
+    }
+}
+
+template <typename T, int BM, int BN, int WM, int WN, int NS, int SM>
+static void launch_pipe_prio(hipStream_t s, int epi, const GemmArgs& a) {
+    const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
+    dim3 grid(nwg), block(64 * WM * WN);
+    switch (epi) {
+        case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE, SM, 0, 1><<<grid, block, 0, s>>>(a); break;
+        case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU, SM, 0, 1><<<grid, block, 0, s>>>(a); break;
+        case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID, SM, 0, 1><<<grid, block, 0, s>>>(a); break;
+        case EPI_PATCH: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_PATCH, SM, 0, 1><<<grid, block, 0, s>>>(a); break;
+        default: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32, SM, 0, 1><<<grid, block, 0, s>>>(a); break;
     }
 }
 
@@ -1315,6 +1332,19 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         case 85:
             if (a.N % 256) return -1;
             launch_pipe<T, 192, 256, 2, 4, 2, 3>(s, epi, a);
+            return 0;
+        // s_setprio(1) around the MFMA clusters of 80 / 13 / 82
+        case 86:
+            if (a.N % 256) return -1;
+            launch_pipe_prio<T, 256, 256, 2, 4, 2, 3>(s, epi, a);
+            return 0;
+        case 87:
+            if (a.N % 128) return -1;
+            launch_pipe_prio<T, 128, 128, 4, 2, 2, 0>(s, epi, a);
+            return 0;
+        case 88:
+            if (a.N % 128) return -1;
+            launch_pipe_prio<T, 160, 128, 2, 2, 2, 3>(s, epi, a);
             return 0;
         case 50:
             if (a.N % 256) return -1;
