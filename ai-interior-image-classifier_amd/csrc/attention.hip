@@ -181,12 +181,14 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // QW waves per workgroup = 16 QW queries; every wave loads 64 / QW key rows of K and of V
 // per block (QW = 8 halves the K/V re-reads of long sequences: the fill path bounds them).
-template <typename T, int QW = 4>
-__global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __restrict__ qkv,
-                                                               u16* __restrict__ out, int N, int H) {
+// SINGLE (N <= 64, the B/32 shape): one key block, one LDS stage, no loop state — fewer live
+// registers, so more workgroups per CU hide the load latency.
+template <typename T, int QW = 4, bool SINGLE = false>
+__global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(const u16* __restrict__ qkv,
+                                                                                u16* __restrict__ out, int N, int H) {
     typedef typename T::vec8 vec8;
     constexpr int STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[(SINGLE ? 1 : 2) * STAGE];
 
     const int D = H * 64;
     const int ld = 3 * D;
@@ -224,10 +226,10 @@ __global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __rest
     for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
     const float scale = 0.125f;  // 1/sqrt(64)
-    const int nkb = (N + 63) >> 6;
+    const int nkb = SINGLE ? 1 : (N + 63) >> 6;
 
     issue(0, 0);
-    if (nkb > 1) issue(1, 1);
+    if (!SINGLE && nkb > 1) issue(1, 1);
     for (int kb = 0; kb < nkb; ++kb) {
         const int st = kb & 1;
         if (kb + 1 < nkb) vm_wait<LPB>();  // block kb landed (this wave's part); kb+1 may fly
@@ -276,14 +278,14 @@ __global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __rest
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] *= alpha;
 
-        // V^T fragments: all 16 transposed reads first (inline asm: a builtin tr-read makes
-        // hipcc drain vmcnt(0) before it, i.e. wait for the NEXT block's glds), then one
-        // lgkmcnt(0) + sched_barrier (hipcc would otherwise hoist the MFMAs past the wait)
+        // V^T fragments by transposed reads (inline asm: a builtin tr-read makes hipcc drain
+        // vmcnt(0) before it, i.e. wait for the NEXT block's glds), then lgkmcnt(0) +
+        // sched_barrier (hipcc would otherwise hoist the MFMAs past the wait)
         const int tq = (lane & 15) >> 2, tp = lane & 3;  // lane 4q + p of its 16-lane group
         const unsigned vbase = (unsigned)(size_t)(LDS_AS const unsigned char*)Vs;
-        u32x2 vr[2][4][2];
 #pragma unroll
-        for (int stp = 0; stp < 2; ++stp)
+        for (int stp = 0; stp < 2; ++stp) {  // one 32-key step at a time: 16 live V registers
+            u32x2 vr[4][2];
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -291,12 +293,8 @@ __global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __rest
                     const int k = 32 * stp + 16 * hf + 4 * g + tq;  // this lane's key row
                     const int cl = 2 * dt + (tp >> 1);               // logical chunk of d = 16 dt + 4 p
                     const unsigned addr = vbase + k * 128 + ((cl ^ (k & 7)) << 4) + 8 * (tp & 1);
-                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[stp][dt][hf]) : "v"(addr) : "memory");
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[dt][hf]) : "v"(addr) : "memory");
                 }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int stp = 0; stp < 2; ++stp) {
             vec8 pf;
             {
                 unsigned w[4] = {pack2<T>(s[2 * stp][0], s[2 * stp][1]), pack2<T>(s[2 * stp][2], s[2 * stp][3]),
@@ -304,13 +302,15 @@ __global__ __launch_bounds__(64 * QW) void attention_v2_kernel(const u16* __rest
                                  pack2<T>(s[2 * stp + 1][2], s[2 * stp + 1][3])};
                 pf = __builtin_bit_cast(vec8, *(uint4*)w);
             }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt) {
-                const uint4 vv = make_uint4(vr[stp][dt][0].x, vr[stp][dt][0].y, vr[stp][dt][1].x, vr[stp][dt][1].y);
+                const uint4 vv = make_uint4(vr[dt][0].x, vr[dt][0].y, vr[dt][1].x, vr[dt][1].y);
                 o[dt] = T::mfma16(__builtin_bit_cast(vec8, vv), pf, o[dt]);
             }
         }
-        if (kb + 2 < nkb) {
+        if (!SINGLE && kb + 2 < nkb) {
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of the stage done
             __builtin_amdgcn_s_barrier();        // ... every wave's
             issue(kb + 2, st);
@@ -354,6 +354,11 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
             attention_v2_kernel<F16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else
             attention_v2_kernel<BF16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v2() && N <= 64) {
+        if (dtype == 2)
+            attention_v2_kernel<F16, 4, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v2_kernel<BF16, 4, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else if (attn_v2()) {
         if (dtype == 2)
             attention_v2_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
