@@ -159,12 +159,15 @@ static void text_pack(clipvit_text_handle* h, const std::string& name, void* dst
     launch_pack_weight(nullptr, h->dt, src ? src : h->master[name], dst, (int)sh[0], (int)sh[1], (int)sh[1]);
 }
 
+// variant: the vision roles' pipelined tiles (qkv / fc: 80 / 13, N = 512 roles: 82, 4x2 XCD
+// partition), falling back to the shape-based choice
 static int text_gemm(hipStream_t s, clipvit_text_handle* h, int epi, const void* A, const void* W,
-                     const float* bias, void* C, int M, int N, int K) {
+                     const float* bias, void* C, int M, int N, int K, int variant) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
-    if (launch_gemm(s, h->dt, epi, a, 0) != 0)
+    a.xcd_n = 2;
+    if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0)
         TFAIL(CLIPVIT_E_INVALID, "text gemm: unsupported shape M=" + std::to_string(M) +
                                      " N=" + std::to_string(N) + " K=" + std::to_string(K));
     return 0;
@@ -343,12 +346,12 @@ int clipvit_encode_text(clipvit_text_handle* h, void* stream, const int32_t* tok
     int rc = 0;
     for (int i = 0; i < h->cfg.layers && !rc; ++i) {
         const TextLayer& ly = h->layers[i];
-        if ((rc = text_gemm(s, h, EPI_STORE, h->h, ly.wqkv, ly.bqkv, h->qkv, M, 3 * D, D))) break;
+        if ((rc = text_gemm(s, h, EPI_STORE, h->h, ly.wqkv, ly.bqkv, h->qkv, M, 3 * D, D, 80))) break;
         launch_attention(s, h->dt, h->qkv, h->h, B, ctx, h->cfg.heads, /*causal=*/true);
-        if ((rc = text_gemm(s, h, EPI_RESID, h->h, ly.wout, ly.bout, h->x, M, D, D))) break;
+        if ((rc = text_gemm(s, h, EPI_RESID, h->h, ly.wout, ly.bout, h->x, M, D, D, 82))) break;
         launch_layernorm(s, h->dt, h->x, h->h, ly.ln2g, ly.ln2b, M, D);
-        if ((rc = text_gemm(s, h, EPI_GELU, h->h, ly.wfc, ly.bfc, h->u, M, 4 * D, D))) break;
-        if ((rc = text_gemm(s, h, EPI_RESID, h->u, ly.wproj, ly.bproj, h->x, M, D, 4 * D))) break;
+        if ((rc = text_gemm(s, h, EPI_GELU, h->h, ly.wfc, ly.bfc, h->u, M, 4 * D, D, 13))) break;
+        if ((rc = text_gemm(s, h, EPI_RESID, h->u, ly.wproj, ly.bproj, h->x, M, D, 4 * D, 82))) break;
         if (i + 1 < h->cfg.layers)
             launch_layernorm(s, h->dt, h->x, h->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
     }
