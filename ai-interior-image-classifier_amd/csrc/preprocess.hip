@@ -152,6 +152,42 @@ __global__ __launch_bounds__(256) void resample_h_kernel(const unsigned char* __
     o[2] = clip8(s2);
 }
 
+// Same output, one workgroup per (source row, image): the row's needed byte span is staged in
+// LDS by coalesced loads, then each thread computes output columns from LDS (the per-thread
+// version issues 3 scattered byte loads per tap). Dynamic LDS = span bytes (<= 48 KiB).
+__global__ __launch_bounds__(256) void resample_h_lds_kernel(const unsigned char* __restrict__ rgb,
+                                                             const ImgDesc* __restrict__ descs,
+                                                             const int32_t* __restrict__ plans,
+                                                             unsigned char* __restrict__ inter, int n) {
+    extern __shared__ unsigned char row[];
+    const ImgDesc d = descs[blockIdx.y];
+    const int r = blockIdx.x;
+    if (r >= d.R) return;
+    const int x0 = plans[d.bh + 2 * d.left];
+    const int lc = d.left + n - 1;
+    const int span = (plans[d.bh + 2 * lc] + plans[d.bh + 2 * lc + 1] - x0) * 3;
+    const unsigned char* src = rgb + d.src + ((size_t)(d.rlo + r) * d.W + x0) * 3;
+    for (int i = threadIdx.x; i < span; i += blockDim.x) row[i] = src[i];
+    __syncthreads();
+    unsigned char* o = inter + d.inter + (size_t)r * n * 3;
+    for (int c = threadIdx.x; c < n; c += blockDim.x) {
+        const int xx = d.left + c;
+        const int xmin = plans[d.bh + 2 * xx], xmax = plans[d.bh + 2 * xx + 1];
+        const int32_t* k = plans + d.kh + (size_t)xx * d.ksh;
+        const unsigned char* sp = row + (xmin - x0) * 3;
+        int s0 = 1 << (PRECISION_BITS - 1), s1 = s0, s2 = s0;
+        for (int x = 0; x < xmax; ++x) {
+            const int w = k[x];
+            s0 += (int)sp[3 * x] * w;
+            s1 += (int)sp[3 * x + 1] * w;
+            s2 += (int)sp[3 * x + 2] * w;
+        }
+        o[3 * c] = clip8(s0);
+        o[3 * c + 1] = clip8(s1);
+        o[3 * c + 2] = clip8(s2);
+    }
+}
+
 template <int OUT>  // 0 fp32, 1 bf16, 2 fp16
 __global__ __launch_bounds__(256) void resample_v_kernel(const ImgDesc* __restrict__ descs,
                                                          const int32_t* __restrict__ plans,
@@ -219,7 +255,7 @@ int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit
     std::vector<ImgDesc> descs((size_t)B);
     std::vector<int32_t> plans;
     long long inter_bytes = 0;
-    int maxR = 0;
+    int maxR = 0, maxSpan = 0;
     // plans depend only on (source size, resized size): one copy per distinct axis pair (a
     // batch of same-size photos uploads two plans, not 2 B)
     struct PlanRef { int b, k, ks, first; };
@@ -257,6 +293,11 @@ int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit
         d.inter = inter_bytes;
         inter_bytes += (long long)d.R * n_px * 3;
         maxR = std::max(maxR, d.R);
+        {
+            const int lc = d.left + n_px - 1;
+            const int span = (plans[ph.b + 2 * lc] + plans[ph.b + 2 * lc + 1] - plans[ph.b + 2 * d.left]) * 3;
+            maxSpan = std::max(maxSpan, span);
+        }
         d.bh = ph.b;
         d.kh = ph.k;
         d.bv = pv.b;
@@ -281,8 +322,13 @@ int clipvit_preprocess(void* stream, const unsigned char* rgb_dev, const clipvit
     const int32_t* dplans = (const int32_t*)((char*)blk + poff);
     unsigned char* dinter = (unsigned char*)blk + ioff;
     if (e == hipSuccess) {
-        dim3 gh((unsigned)(((long long)maxR * n_px + 255) / 256), (unsigned)B);
-        resample_h_kernel<<<gh, 256, 0, s>>>(rgb_dev, ddesc, dplans, dinter, n_px);
+        if (maxSpan <= 48 * 1024) {
+            resample_h_lds_kernel<<<dim3((unsigned)maxR, (unsigned)B), 256, maxSpan, s>>>(rgb_dev, ddesc, dplans,
+                                                                                     dinter, n_px);
+        } else {
+            dim3 gh((unsigned)(((long long)maxR * n_px + 255) / 256), (unsigned)B);
+            resample_h_kernel<<<gh, 256, 0, s>>>(rgb_dev, ddesc, dplans, dinter, n_px);
+        }
         dim3 gv((unsigned)((n_px * n_px + 255) / 256), (unsigned)B);
         if (out_dtype == CLIPVIT_F32) resample_v_kernel<0><<<gv, 256, 0, s>>>(ddesc, dplans, dinter, out_dev, n_px);
         else if (out_dtype == CLIPVIT_BF16) resample_v_kernel<1><<<gv, 256, 0, s>>>(ddesc, dplans, dinter, out_dev, n_px);
