@@ -134,6 +134,8 @@ struct clipvit_handle {
     // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
     // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles)
     int var[5] = {80, 82, 13, 82, 22};
+    bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
+    int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
     int xcd[5] = {2, 2, 2, 2, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
@@ -274,7 +276,16 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
-    const int variant = h->var[role];
+    int variant = h->var[role];
+    // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
+    // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
+    // lower LDS fill per FLOP wins — measured: config 4 1,918 -> 2,072 img/s; B/16 c_fc (2,364
+    // tiles) and out/c_proj (591 tiles, N = 768 roles from 2 rounds) 19.3k -> 20.2k img/s;
+    // B/32's c_fc (600 tiles) stays faster on 128x128.
+    const long t256 = N % 256 == 0 ? (long)((M + 255) / 256) * (N / 256) : 0;
+    if (!h->var_forced && role != R_PATCH &&
+        (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu)))
+        variant = 80;
     // a tuned variant that does not tile this shape falls back to the shape-based choice
     if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -632,7 +643,13 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
             if (*p == ',') ++p;
         }
     }
+    {
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            h->ncu = ncu;
+    }
     if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
+        h->var_forced = true;
         int k = 0;
         for (const char* p = v; *p && k < 5; ++k) {
             h->var[k] = atoi(p);
