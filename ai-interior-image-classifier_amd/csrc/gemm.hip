@@ -1333,6 +1333,16 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 256) return -1;
             launch_pipe<T, 192, 256, 2, 4, 2, 3>(s, epi, a);
             return 0;
+        // 64x64 pipelined tiles with deep rings (the class-token tail's M = B GEMMs: few
+        // workgroups, long K, weights cold in cache -> latency-bound; more k-tiles in flight)
+        case 90:
+            if (a.N % 64) return -1;
+            launch_pipe<T, 64, 64, 2, 1, 4>(s, epi, a);
+            return 0;
+        case 91:
+            if (a.N % 64) return -1;
+            launch_pipe<T, 64, 64, 2, 1, 8>(s, epi, a);
+            return 0;
         // s_setprio(1) around the MFMA clusters of 80 / 13 / 82
         case 86:
             if (a.N % 256) return -1;
