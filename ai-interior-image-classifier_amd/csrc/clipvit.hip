@@ -89,6 +89,8 @@ struct Workspace {
     Lane lane[kLanes];
     hipEvent_t fork = nullptr;
     bool used = false;
+    hipStream_t last_stream = nullptr;  // stream of the last call that used it
+    unsigned long long last_use = 0;    // call counter at that use (LRU)
 };
 
 // F_TAIL: the last block's row-wise part on class-token rows (cls_tail)
@@ -159,6 +161,8 @@ struct clipvit_handle {
     bool defer_x = true;
     // last block on class-token rows only (see cls_tail); CLIPVIT_CLS_PRUNE=0 disables
     bool cls_prune = true;
+    unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
+    int max_inflight = 2;  // workspaces kept for calls in flight on different streams (CLIPVIT_MAX_INFLIGHT)
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
 };
 
@@ -242,25 +246,53 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
 
 // Take a free workspace (allocating one if every pooled workspace is busy). Every use of a
 // lane's buffers is ordered after the previous one through the lane's `done` event.
+// True when every lane's last recorded GPU work has finished (a call taking it will not wait).
+static bool ws_idle(const Workspace* w) {
+    for (const auto& l : w->lane)
+        if (hipEventQuery(l.done) != hipSuccess) return false;
+    return true;
+}
+
+// Take a workspace for one call. Preference: a free one whose previous GPU work is done; then,
+// while the pool is below max_inflight, a new one — so calls issued on different streams
+// (batches in flight, e.g. bench.py alternating two streams) do not serialise on one
+// workspace's events; otherwise any free one (the call is ordered after its previous user
+// through the lanes' `done` events). With every workspace held by a concurrent host call, a
+// new one is allocated (the reference's ThreadPoolExecutor pattern).
 static int acquire_ws(clipvit_handle* h, hipStream_t s, Workspace** out) {
     Workspace* w = nullptr;
+    bool grow = false;
     {
         std::lock_guard<std::mutex> lk(h->mu);
-        for (auto* c : h->pool)
-            if (c && !c->used) {
+        Workspace *same = nullptr, *lru = nullptr;
+        for (auto* c : h->pool) {
+            if (!c || c->used) continue;
+            if (ws_idle(c)) {
                 w = c;
                 break;
             }
+            if (c->last_stream == s && (!same || c->last_use > same->last_use)) same = c;
+            if (!lru || c->last_use < lru->last_use) lru = c;
+        }
+        // busy on the GPU: the caller's own stream orders it for free; otherwise grow up to
+        // max_inflight before waiting on another stream's work (least recently used)
+        if (!w) w = same;
+        if (!w && (int)h->pool.size() >= h->max_inflight) w = lru;
         if (w) w->used = true;
+        else grow = true;
     }
-    if (!w) {
+    if (grow) {
         int rc = alloc_ws(h, &w);
         if (rc) return rc;
         w->used = true;
         std::lock_guard<std::mutex> lk(h->mu);
         h->pool.push_back(w);
     }
-    (void)s;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        w->last_stream = s;
+        w->last_use = ++h->calls;
+    }
     *out = w;
     return 0;
 }
@@ -613,6 +645,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
+    if (const char* v = getenv("CLIPVIT_MAX_INFLIGHT")) h->max_inflight = std::max(1, atoi(v));
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;

@@ -56,6 +56,7 @@ def parse():
                    help="MFMA operand type; fp16 meets the 1e-3 logit bar, bf16 does not (DESIGN.md); "
                         "mxfp8 = BASELINE config 5 (MX-fp8 Linears, bf16 attention; bar 2e-2 vs bf16)")
     p.add_argument("--lora-rank", type=int, default=8)
+    p.add_argument("--inflight", type=int, default=1, help="batches in flight on separate HIP streams")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-iters", type=int, default=5)
@@ -127,12 +128,24 @@ def main():
     eng.set_text_features(T.numpy(), SEGMENTS)
     gpx = torch.Generator(device=dev).manual_seed(100 + rank)
     px = torch.randn(a.batch, 3, cfg.image_size, cfg.image_size, device=dev, generator=gpx).clamp_(-1.8, 2.2)
-    out = eng.classify(px)   # allocates the output buffers once
+    # --inflight batches in flight: step i runs on stream i % n with its own output buffers (the
+    # handle hands each in-flight call its own workspace), so one batch's latency-bound tail
+    # (class-token block, head) overlaps the next batch's GEMMs. Every step is still one whole
+    # batch through the whole path; the timed region brackets all streams.
+    # (non-default streams: the legacy default stream would order itself against the others)
+    streams = [torch.cuda.Stream(dev) for _ in range(max(1, a.inflight))]
+    outs = [eng.classify(px) for _ in streams]   # allocates the output buffers once
+    out = outs[0]
+    torch.cuda.synchronize()
+    it = [0]
 
     def step():
-        eng.classify(px, out)
-        if world > 1:
-            allgather_rows(out.logits)
+        j = it[0] % len(streams)
+        it[0] += 1
+        with torch.cuda.stream(streams[j]):
+            eng.classify(px, outs[j])
+            if world > 1:
+                allgather_rows(outs[j].logits)
 
     for _ in range(a.warmup):
         step()
@@ -183,7 +196,8 @@ def main():
         "data": "synthetic (seeded N(0,1) pixels clamped to CLIP-normalised range, seeded CLIP-style weights, synthetic unit text features)",
         "config": {"workload": f"{cfg.name} + merged LoRA r={a.lora_rank} classify (encode_image + cosine head over {N_CLASSES} labels, 6 segments)",
                    "image_size": cfg.image_size, "per_gpu_batch": a.batch, "global_batch": a.batch * world,
-                   "parallelism": f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else "")},
+                   "parallelism": f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else ""),
+                   "batches_in_flight": a.inflight},
         "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj)",
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),

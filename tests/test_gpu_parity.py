@@ -192,6 +192,30 @@ def test_pixel_dtype_16bit_input_is_bit_identical(gpu, dtype, pdt):
     assert torch.equal(a, b)
 
 
+def test_batches_in_flight_on_two_streams(gpu):
+    """bench.py keeps two batches in flight on two HIP streams; the handle gives the second
+    in-flight call its own workspace. Outputs equal the single-stream outputs bit for bit."""
+    cfg = C.VIT_B32
+    sd = synthetic_state_dict(cfg, 0)
+    T = _text(cfg.embed_dim, 437)
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    eng = VisionEngine(cfg, 0, "fp16", max_batch=128)
+    eng.load_state_dict(sd)
+    eng.set_text_features(T.numpy(), seg)
+    pxs = [_pixels(96, 224, seed=31 + i).to(gpu) for i in range(4)]
+    ref = [eng.classify(p).logits.clone() for p in pxs]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)]
+    outs = [None] * 4
+    for i, p in enumerate(pxs):
+        with torch.cuda.stream(streams[i % 2]):
+            outs[i] = eng.classify(p)
+    torch.cuda.synchronize()
+    for r, o in zip(ref, outs):
+        assert torch.equal(r, o.logits)
+    eng.close()
+
+
 def test_concurrent_host_threads(gpu):
     """The reference calls encode_image from ThreadPoolExecutor(4) (main.py:345-346); the
     handle must give every thread its own workspace and correct results."""
