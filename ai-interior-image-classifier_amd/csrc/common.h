@@ -154,15 +154,24 @@ struct GemmArgs {
 };
 
 // Map a launch-order block id to its (m-tile, n-tile). Blocks b, b+8, ... are observed to
-// share an XCD (speed only, never correctness). With xn == 2 the 8 XCD groups form a 4 x 2
-// grid over (M, N): each group streams its M-band's A panels once and keeps HALF of W in its
-// 4 MB L2; tiles inside a group run M-major. Returns false for padding blocks.
+// share an XCD (speed only, never correctness). A 2-D partition gives every XCD group one cell
+// of an XM x XN grid over (M-tiles, N-tiles): the group streams its M-band's A panels and keeps
+// its share of W in its 4 MB L2; tiles inside a group run M-major. xn selects the grid:
+// 2 = 4 x 2, 4 = 2 x 4, 8 = 1 x 8, 16 = 8 x 1 (XN must divide the N-tile count, else the 1-D
+// bijective remap: each group takes a contiguous range of the row-major tile order).
+__host__ __device__ inline int xcd_split_n(int nN, int xn) {
+    const int XN = xn == 16 ? 1 : xn;
+    return (xn == 2 || xn == 4 || xn == 8 || xn == 16) && nN % XN == 0 ? XN : 0;
+}
+
 __device__ __forceinline__ bool tile_of_block(int bid, int nM, int nN, int xn, int& mt, int& nt) {
-    if (xn == 2 && (nN & 1) == 0) {
+    const int XN = xcd_split_n(nN, xn);
+    if (XN) {
+        const int XM = 8 / XN;
         const int x = bid & 7, j = bid >> 3;
-        const int xm = x >> 1, xh = x & 1;
-        const int m_lo = (nM * xm) >> 2, m_hi = (nM * (xm + 1)) >> 2;
-        const int n_lo = xh * (nN >> 1), nr = nN >> 1;
+        const int xm = x / XN, xh = x % XN;
+        const int m_lo = (nM * xm) / XM, m_hi = (nM * (xm + 1)) / XM;
+        const int nr = nN / XN, n_lo = xh * nr;
         if (j >= (m_hi - m_lo) * nr) return false;
         mt = m_lo + j / nr;
         nt = n_lo + j % nr;
@@ -177,15 +186,17 @@ __device__ __forceinline__ bool tile_of_block(int bid, int nM, int nN, int xn, i
     return true;
 }
 
-// Grid size matching tile_of_block: 8 x (largest group) for the 2-D partition.
+// Grid size matching tile_of_block: 8 x (largest group) for a 2-D partition.
 __host__ __device__ inline int grid_for(int nM, int nN, int xn) {
-    if (xn == 2 && (nN & 1) == 0) {
+    const int XN = xcd_split_n(nN, xn);
+    if (XN) {
+        const int XM = 8 / XN;
         int mx = 0;
-        for (int xm = 0; xm < 4; ++xm) {
-            const int rows = ((nM * (xm + 1)) >> 2) - ((nM * xm) >> 2);
+        for (int xm = 0; xm < XM; ++xm) {
+            const int rows = ((nM * (xm + 1)) / XM) - ((nM * xm) / XM);
             mx = rows > mx ? rows : mx;
         }
-        return 8 * mx * (nN >> 1);
+        return 8 * mx * (nN / XN);
     }
     return nM * nN;
 }
