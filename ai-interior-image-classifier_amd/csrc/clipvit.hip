@@ -134,7 +134,9 @@ struct clipvit_handle {
     std::vector<Workspace*> pool;
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from in-model sweeps on MI355X
     // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
-    // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles)
+    // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles). The 224x192
+    // one-round tiles 92 / 93 win standalone (c_proj 67.4 -> 62.7 us, patch 75.2 -> 69.6) but
+    // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158)
     int var[5] = {80, 82, 13, 82, 22};
     bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
     int ncu = 256;            // compute units of the device
@@ -164,6 +166,8 @@ struct clipvit_handle {
     unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
     int max_inflight = 2;  // workspaces kept for calls in flight on different streams (CLIPVIT_MAX_INFLIGHT)
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
+    // whole-round row split of the 16-bit-output GEMMs (see gemm()); CLIPVIT_GEMM_SPLIT=0 disables
+    bool round_split = true;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -318,6 +322,32 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // tiles) and out/c_proj (591 tiles, N = 768 roles from 2 rounds) 19.3k -> 20.2k img/s;
     // B/32's c_fc (600 tiles) stays faster on 128x128.
     const long t256 = N % 256 == 0 ? (long)((M + 255) / 256) * (N / 256) : 0;
+    // Whole-round row split (QKV / c_fc, 16-bit outputs). When the 256x256 tiles of a shape fill
+    // R whole rounds of the CUs plus a remainder of at most half a round (B/32 c_fc at bs 256:
+    // 600 tiles = 2 rounds + 88), rows [0, M1) — the most 256-row tiles that fit in R rounds,
+    // 1-D block map so every XCD gets the same tile count — run on 256x256 tiles and rows
+    // [M1, M) on the role's small tile as a second launch. Row-wise independent outputs:
+    // bit-identical to one launch. Measured (c_fc 12800 x 3072 x 768): 81.6 us in one launch
+    // (128x128) or 77.6 (256x256, 3 rounds) -> 54.3 + 15.9 = 70.2 us.
+    if (h->round_split && !h->var_forced && (role == R_FC || role == R_QKV) && t256 &&
+        t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
+        const long nN = N / 256, R = t256 / h->ncu, rem = t256 % h->ncu;
+        const long m1 = R * h->ncu / nN * 256;
+        if (R >= 1 && rem > 0 && 2 * rem <= h->ncu && m1 > 0 && m1 < M) {
+            GemmArgs b = a;
+            b.M = (int)m1;
+            b.xcd_n = 0;
+            GemmArgs c = a;
+            c.A = (const unsigned char*)A + (size_t)m1 * K * 2;
+            c.C = (unsigned char*)C + (size_t)m1 * ldc * 2;
+            c.M = M - (int)m1;
+            c.xcd_n = 0;
+            if (launch_gemm(s, h->dt, epi, b, 8) == 0 && launch_gemm(s, h->dt, epi, c, variant) == 0)
+                return 0;
+            g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
+            return CLIPVIT_E_INVALID;
+        }
+    }
     if (!h->var_forced && role != R_PATCH &&
         (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu)))
         variant = 80;
@@ -644,6 +674,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
     if (const char* v = getenv("CLIPVIT_MAX_INFLIGHT")) h->max_inflight = std::max(1, atoi(v));
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {

@@ -1343,6 +1343,26 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 64) return -1;
             launch_pipe<T, 64, 64, 2, 1, 8>(s, epi, a);
             return 0;
+        // 192-wide tiles for the N = 768 roles (out_proj, c_proj, patch): 4 N-tiles, and with
+        // 224 rows 58 x 4 = 232 tiles = ONE round of 256 CUs (160x128: 480 tiles on two
+        // workgroups per CU) at 0.0097 B of LDS fill per FLOP instead of 0.0141. 6 waves (2 x 3,
+        // 128 x 64 or 112 x 64 per wave), 92 / 94 with the LDS-staged 16-bit epilogue.
+        case 92:
+            if (a.N % 192) return -1;
+            launch_pipe<T, 224, 192, 2, 3, 2, 3>(s, epi, a);
+            return 0;
+        case 93:
+            if (a.N % 192) return -1;
+            launch_pipe<T, 224, 192, 2, 3, 2>(s, epi, a);
+            return 0;
+        case 94:
+            if (a.N % 192) return -1;
+            launch_pipe<T, 256, 192, 2, 3, 2, 3>(s, epi, a);
+            return 0;
+        case 95:
+            if (a.N % 192) return -1;
+            launch_pipe<T, 256, 192, 2, 3, 2>(s, epi, a);
+            return 0;
         // s_setprio(1) around the MFMA clusters of 80 / 13 / 82
         case 86:
             if (a.N % 256) return -1;

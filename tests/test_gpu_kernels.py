@@ -30,10 +30,11 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 VARIANTS = list(range(1, 16)) + [21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 34, 40, 41, 42, 43,
                                   50, 51, 52, 53, 70, 71, 80, 81, 82, 208, 213, 221, 222, 230, 250, 251,
                                   252, 270, 280, 281, 282, 83, 84, 85, 283, 86, 87, 88, 90, 91,
-                                  413, 813, 1613, 1680, 422]
+                                  413, 813, 1613, 1680, 422, 92, 93, 94, 95, 292, 293]
 N128 = (1, 2, 6, 7, 10, 11, 12, 13, 22, 26, 42, 43, 52, 81, 82, 87, 88)
 N256 = (3, 5, 8, 9, 14, 15, 21, 23, 24, 25, 27, 28, 29, 30, 31, 34, 40, 41, 50, 51, 53, 70, 71, 80, 83, 84, 85, 86)
-STAGED = (80, 81, 82, 83, 85, 86, 88)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
+N192 = (92, 93, 94, 95)
+STAGED = (80, 81, 82, 83, 85, 86, 88, 92, 94)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
 PERSIST = (40, 41, 42, 43)  # persistent store-overlapped kernels (gemm_ps.hip)
 DEFER = (30, 31, 34)  # persistent deferred-epilogue kernels: 16-bit outputs, bias, K >= 640
 
@@ -48,7 +49,7 @@ def _tol(variant, dtype):
 
 def _skip(variant, N, K):
     v = variant % 100
-    if (v in N128 and N % 128) or (v in N256 and N % 256):
+    if (v in N128 and N % 128) or (v in N256 and N % 256) or (v in N192 and N % 192):
         return "tile does not divide N"
     if v in DEFER and K < 640:
         return "deferred-epilogue kernel needs K >= 640"
@@ -94,10 +95,14 @@ def test_gemm_asymmetric_identity(gpu):
     A = torch.eye(K, device=gpu).to(torch.bfloat16)
     W = (torch.arange(N * K, device=gpu, dtype=torch.float32).reshape(N, K) % 251) / 8.0
     for variant in VARIANTS:
-        if variant % 100 in DEFER:
+        if variant % 100 in DEFER + N192:
             continue
         C = E.gemm_test(A, W, None, epi=0, variant=variant)
         assert torch.equal(C, W.to(torch.bfloat16).float().t()), variant
+    Wr = (torch.arange(384 * K, device=gpu, dtype=torch.float32).reshape(384, K) % 251) / 8.0
+    for variant in N192:
+        C = E.gemm_test(A, Wr, None, epi=0, variant=variant)
+        assert torch.equal(C, Wr.to(torch.bfloat16).float().t()), variant
 
 
 @pytest.mark.parametrize("variant", [30, 31, 34, 230])
