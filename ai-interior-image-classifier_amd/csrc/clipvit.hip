@@ -168,6 +168,7 @@ struct clipvit_handle {
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
     // whole-round row split of the 16-bit-output GEMMs (see gemm()); CLIPVIT_GEMM_SPLIT=0 disables
     bool round_split = true;
+    int split_main = 8, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
 };
 
 static std::string L(int i, const char* leaf) {
@@ -342,7 +343,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             c.C = (unsigned char*)C + (size_t)m1 * ldc * 2;
             c.M = M - (int)m1;
             c.xcd_n = 0;
-            if (launch_gemm(s, h->dt, epi, b, 8) == 0 && launch_gemm(s, h->dt, epi, c, variant) == 0)
+            if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 &&
+                launch_gemm(s, h->dt, epi, c, h->split_tail ? h->split_tail : variant) == 0)
                 return 0;
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
@@ -675,6 +677,10 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {
+        h->split_main = atoi(v);
+        if (const char* c = strchr(v, ',')) h->split_tail = atoi(c + 1);
+    }
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
     if (const char* v = getenv("CLIPVIT_MAX_INFLIGHT")) h->max_inflight = std::max(1, atoi(v));
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
