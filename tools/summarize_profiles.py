@@ -27,6 +27,12 @@ def roles_for_trace(rows):
     """Assign a role to every dispatch of the encoder forward, by order."""
     out = []
     layer_seq = ["qkv", "attention", "out", "ln2", "fc", "proj", "ln1"]
+    # c_fc runs as two launches (whole-round row split, DESIGN.md §11) when the dispatch count
+    # between two attention kernels is 8: main rows then tail rows
+    att = [i for i, r in enumerate(rows) if "attention" in r["Kernel_Name"]][:2]
+    if len(att) == 2 and att[1] - att[0] == 8:
+        layer_seq = ["qkv", "attention", "out", "ln2", "fc", "fc_tail", "proj", "ln1"]
+    L = len(layer_seq)
     pos = None
     for r in rows:
         n = r["Kernel_Name"]
@@ -47,7 +53,7 @@ def roles_for_trace(rows):
         if "seg_softmax" in n:
             out.append("head_softmax"); continue
         if isinstance(pos, int) and (gemm_like(n) or "attention" in n or "layernorm" in n):
-            out.append(layer_seq[pos % 7]); pos += 1; continue
+            out.append(layer_seq[pos % L]); pos += 1; continue
         out.append("other")
     return out
 
@@ -96,6 +102,12 @@ def main():
         wb = sum(write[role]) / len(write[role]) * 1024 / 1e6 if write.get(role) else float("nan")
         traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6}
         lines.append(f"| {role} | {len(d)} | {avg:.1f} | {tf} | {fb:.1f} | {wb:.1f} |")
+    if "fc_tail" in traffic:  # one c_fc invocation = main + tail launch
+        a, b = traffic["fc"], traffic.pop("fc_tail")
+        traffic["fc"] = {k: a[k] + b[k] for k in a}
+        t = traffic["fc"]
+        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {flops['fc'] / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
+                     f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     mlp = [traffic[r] for r in ("fc", "proj") if r in traffic]
     entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
