@@ -332,6 +332,182 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
     }
 }
 
+// attention_v3_kernel: attention_v2's algorithm with 16 QF queries per wave (QF 16-query
+// fragments f; QF = 2 or 4). Every K fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16)
+// read from LDS feeds two MFMAs instead of one, which halves the LDS read bytes per FLOP: at
+// 16 queries per wave v2 reads 32 KB of LDS per 32 MFMAs per SIMD, the LDS array's peak.
+// QW waves = 32 QW queries per workgroup; SINGLE as in v2 (N <= 64: one key block, one stage).
+template <typename T, int QW = 4, bool SINGLE = false, int QF = 2>
+__global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(const u16* __restrict__ qkv,
+                                                                                u16* __restrict__ out, int N, int H) {
+    typedef typename T::vec8 vec8;
+    constexpr int STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
+    __shared__ __attribute__((aligned(16))) unsigned char smem[(SINGLE ? 1 : 2) * STAGE];
+
+    const int D = H * 64;
+    const int ld = 3 * D;
+    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, g = lane >> 4;
+    const size_t base = (size_t)b * N;
+
+    int q[QF];
+    vec8 qf[QF][2];
+#pragma unroll
+    for (int f = 0; f < QF; ++f) {
+        q[f] = qb * (16 * QF * QW) + wave * (16 * QF) + f * 16 + j;
+        const u16* qrow = qkv + (base + min(q[f], N - 1)) * ld + h * 64;
+        qf[f][0] = *(const vec8*)(qrow + 8 * g);
+        qf[f][1] = *(const vec8*)(qrow + 32 + 8 * g);
+    }
+
+    constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
+    const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
+    auto issue = [&](int kb, int st) {
+        unsigned char* dst = smem + st * STAGE;
+#pragma unroll
+        for (int r = 0; r < RW / 8; ++r) {
+            const int row = wave * RW + r * 8 + (lane >> 3);
+            const int key = min(kb * 64 + row, N - 1);
+            const int c = (lane & 7) ^ (row & 7);
+            const unsigned char* ks = src + (size_t)key * ld * 2 + c * 16;
+            glds16(ks, dst + (wave * RW + r * 8) * 128);
+            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * RW + r * 8) * 128);
+        }
+    };
+
+    f32x4 o[QF][4];
+#pragma unroll
+    for (int f = 0; f < QF; ++f)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[f][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run[QF], l_run[QF];
+#pragma unroll
+    for (int f = 0; f < QF; ++f) { m_run[f] = -INFINITY; l_run[f] = 0.f; }
+    const float scale = 0.125f;  // 1/sqrt(64)
+    const int nkb = SINGLE ? 1 : (N + 63) >> 6;
+
+    issue(0, 0);
+    if (!SINGLE && nkb > 1) issue(1, 1);
+    for (int kb = 0; kb < nkb; ++kb) {
+        const int st = kb & 1;
+        if (kb + 1 < nkb) vm_wait<LPB>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        const unsigned char* Ks = smem + st * STAGE;
+        const unsigned char* Vs = Ks + 8192;
+
+        f32x4 s[QF][4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+            for (int f = 0; f < QF; ++f) s[f][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int row = kt * 16 + j;
+#pragma unroll
+            for (int ds = 0; ds < 2; ++ds) {
+                const int c = ((ds << 2) | g) ^ (row & 7);
+                const vec8 kf = *(const vec8*)(Ks + row * 128 + (c << 4));
+#pragma unroll
+                for (int f = 0; f < QF; ++f) s[f][kt] = T::mfma16(kf, qf[f][ds], s[f][kt]);
+            }
+        }
+#pragma unroll
+        for (int f = 0; f < QF; ++f) {
+            float mloc = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int key = kb * 64 + kt * 16 + 4 * g + r;
+                    const float v = key < N ? s[f][kt][r] * scale : -INFINITY;
+                    s[f][kt][r] = v;
+                    mloc = fmaxf(mloc, v);
+                }
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+            const float m_new = fmaxf(m_run[f], mloc);
+            const float alpha = __expf(m_run[f] - m_new);
+            m_run[f] = m_new;
+            float lsum = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float p = __expf(s[f][kt][r] - m_new);
+                    s[f][kt][r] = p;
+                    lsum += p;
+                }
+            l_run[f] = l_run[f] * alpha + lsum;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[f][i] *= alpha;
+        }
+
+        const int tq = (lane & 15) >> 2, tp = lane & 3;
+        const unsigned vbase = (unsigned)(size_t)(LDS_AS const unsigned char*)Vs;
+#pragma unroll
+        for (int stp = 0; stp < 2; ++stp) {
+            u32x2 vr[4][2];
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const int k = 32 * stp + 16 * hf + 4 * g + tq;
+                    const int cl = 2 * dt + (tp >> 1);
+                    const unsigned addr = vbase + k * 128 + ((cl ^ (k & 7)) << 4) + 8 * (tp & 1);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[dt][hf]) : "v"(addr) : "memory");
+                }
+            vec8 pf[QF];
+#pragma unroll
+            for (int f = 0; f < QF; ++f) {
+                unsigned w[4] = {pack2<T>(s[f][2 * stp][0], s[f][2 * stp][1]), pack2<T>(s[f][2 * stp][2], s[f][2 * stp][3]),
+                                 pack2<T>(s[f][2 * stp + 1][0], s[f][2 * stp + 1][1]),
+                                 pack2<T>(s[f][2 * stp + 1][2], s[f][2 * stp + 1][3])};
+                pf[f] = __builtin_bit_cast(vec8, *(uint4*)w);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const uint4 vv = make_uint4(vr[dt][0].x, vr[dt][0].y, vr[dt][1].x, vr[dt][1].y);
+#pragma unroll
+                for (int f = 0; f < QF; ++f) o[f][dt] = T::mfma16(__builtin_bit_cast(vec8, vv), pf[f], o[f][dt]);
+            }
+        }
+        if (!SINGLE && kb + 2 < nkb) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_s_barrier();
+            issue(kb + 2, st);
+        }
+    }
+
+#pragma unroll
+    for (int f = 0; f < QF; ++f) {
+        float l = l_run[f];
+        l += __shfl_xor(l, 16, 64);
+        l += __shfl_xor(l, 32, 64);
+        if (q[f] < N) {
+            const float inv = 1.0f / l;
+            u16* orow = out + (base + q[f]) * D + h * 64;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                uint2 w;
+                w.x = pack2<T>(o[f][dt][0] * inv, o[f][dt][1] * inv);
+                w.y = pack2<T>(o[f][dt][2] * inv, o[f][dt][3] * inv);
+                *(uint2*)(orow + dt * 16 + 4 * g) = w;
+            }
+        }
+    }
+}
+
+static int attn_v3() {  // CLIPVIT_ATTN_V3: 0 off, 1 (default) long sequences, 2 also N <= 64, 3 = 1 with 64 queries per wave
+    static const int on = [] {
+        const char* v = getenv("CLIPVIT_ATTN_V3");
+        return v ? atoi(v) : 1;
+    }();
+    return on;
+}
+
 static bool attn_v2() {
     static const bool on = [] {
         const char* v = getenv("CLIPVIT_ATTN_V2");
@@ -348,6 +524,23 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
             attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else
             attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v3() == 3 && N > 128) {  // long sequences: 2 waves x 64 queries
+        dim3 g4((N + 127) / 128, H, B);
+        if (dtype == 2)
+            attention_v3_kernel<F16, 2, false, 4><<<g4, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v3_kernel<BF16, 2, false, 4><<<g4, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v3() >= 1 && N > 128) {  // long sequences: 4 waves x 32 queries
+        dim3 g4((N + 127) / 128, H, B);
+        if (dtype == 2)
+            attention_v3_kernel<F16, 4><<<g4, 256, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v3_kernel<BF16, 4><<<g4, 256, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (attn_v3() >= 2 && N <= 64) {  // one key block: 2 waves x 32 queries
+        if (dtype == 2)
+            attention_v3_kernel<F16, 2, true><<<grid, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v3_kernel<BF16, 2, true><<<grid, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else if (attn_v2() && N > 128) {  // long sequences: 128 queries per workgroup
         dim3 g8((N + 127) / 128, H, B);
         if (dtype == 2)
