@@ -1363,6 +1363,17 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 192) return -1;
             launch_pipe<T, 256, 192, 2, 3, 2>(s, epi, a);
             return 0;
+        // 32x64 tiles of ONE wave (class-token tail, M = B rows): twice the workgroups of 64x64
+        // and 0.75x the LDS fill bytes per tile, since the tail's long-K GEMMs are bound by
+        // the per-CU fill rate on few CUs; 4- / 8-stage ring
+        case 96:
+            if (a.N % 64) return -1;
+            launch_pipe<T, 32, 64, 1, 1, 4>(s, epi, a);
+            return 0;
+        case 97:
+            if (a.N % 64) return -1;
+            launch_pipe<T, 32, 64, 1, 1, 8>(s, epi, a);
+            return 0;
         // s_setprio(1) around the MFMA clusters of 80 / 13 / 82
         case 86:
             if (a.N % 256) return -1;
