@@ -136,8 +136,10 @@ struct clipvit_handle {
     // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
     // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles). The 224x192
     // one-round tiles 92 / 93 win standalone (c_proj 67.4 -> 62.7 us, patch 75.2 -> 69.6) but
-    // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158)
-    int var[5] = {80, 82, 13, 82, 22};
+    // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158).
+    // 98 = 240x256 QKV tiles of 12 waves (486 tiles = 1.9 rounds at bs 256 against 450 = 1.76
+    // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward (tools/exp_qkv240.sh)
+    int var[5] = {98, 82, 13, 82, 22};
     bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid

@@ -1374,6 +1374,18 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 64) return -1;
             launch_pipe<T, 32, 64, 1, 1, 8>(s, epi, a);
             return 0;
+        // 240x256 tiles for QKV (N = 2304 = 9 x 256): M = 12800 -> 54 M-tiles, 486 tiles =
+        // 1.9 rounds of 256 CUs at 0.94x the work per tile, against 450 = 1.76 rounds of
+        // 256x256 (whose second round is a full tile time). 98: 12 waves (3 x 4, 80 x 64 per
+        // wave: three waves on every SIMD); 99: 6 waves (3 x 2, 80 x 128). LDS-staged epilogue.
+        case 98:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);
+            return 0;
+        case 99:
+            if (a.N % 256) return -1;
+            launch_pipe<T, 240, 256, 3, 2, 2, 3>(s, epi, a);
+            return 0;
         // s_setprio(1) around the MFMA clusters of 80 / 13 / 82
         case 86:
             if (a.N % 256) return -1;
