@@ -167,42 +167,62 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // x[row] += y[row] (16-bit branch output of out_proj / c_proj); h[row] = LayerNorm(x[row]).
 // Moves the residual add out of the GEMM epilogue (which then only stores y): the GEMM no
 // longer reads x, and this kernel streams x, y -> x, h in one pass.
-template <typename T, int V, bool STORE_X = true, bool TWO = false>
+template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
                                                             u16* __restrict__ h, const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
+    // RPW rows per wave, every row's loads issued before any row's arithmetic (more bytes in
+    // flight per wave; rows / RPW waves fit one residency round of the CUs at bs 256)
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= rows) return;
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    if (row0 >= rows) return;
     constexpr int D = 256 * V;
-    float* xr = x + (size_t)row * D;
-    const u16* yr = y + (size_t)row * D;
-    float4 v[V];
-    uint2 w[V], w2[V];
+    float4 v[RPW][V];
+    uint2 w[RPW][V], w2[RPW][V];
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-        v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
-        w[i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
-        if constexpr (TWO) w2[i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
-    }
+    for (int r = 0; r < RPW; ++r) {
+        const int row = min(row0 + r, rows - 1);
+        const float* xr = x + (size_t)row * D;
+        const u16* yr = y + (size_t)row * D;
 #pragma unroll
-    for (int i = 0; i < V; ++i) {
-        // (x + y) + y2: the same fp32 additions, in the same order, as two separate residual adds
-        v[i].x += T::to_f32((u16)(w[i].x & 0xffff));
-        v[i].y += T::to_f32((u16)(w[i].x >> 16));
-        v[i].z += T::to_f32((u16)(w[i].y & 0xffff));
-        v[i].w += T::to_f32((u16)(w[i].y >> 16));
-        if constexpr (TWO) {
-            v[i].x += T::to_f32((u16)(w2[i].x & 0xffff));
-            v[i].y += T::to_f32((u16)(w2[i].x >> 16));
-            v[i].z += T::to_f32((u16)(w2[i].y & 0xffff));
-            v[i].w += T::to_f32((u16)(w2[i].y >> 16));
+        for (int i = 0; i < V; ++i) {
+            v[r][i] = *(const float4*)(xr + (lane + 64 * i) * 4);
+            w[r][i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
+            if constexpr (TWO) w2[r][i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
         }
-        if constexpr (STORE_X) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
     }
-    ln_row<V>(v, gm, bt, lane, (float)D);
-    store_row16<T, V>(h + (size_t)row * D, v, lane);
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int row = row0 + r;
+        if (row >= rows) break;
+        float* xr = x + (size_t)row * D;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            // (x + y) + y2: the same fp32 additions, in the same order, as two separate residual adds
+            v[r][i].x += T::to_f32((u16)(w[r][i].x & 0xffff));
+            v[r][i].y += T::to_f32((u16)(w[r][i].x >> 16));
+            v[r][i].z += T::to_f32((u16)(w[r][i].y & 0xffff));
+            v[r][i].w += T::to_f32((u16)(w[r][i].y >> 16));
+            if constexpr (TWO) {
+                v[r][i].x += T::to_f32((u16)(w2[r][i].x & 0xffff));
+                v[r][i].y += T::to_f32((u16)(w2[r][i].x >> 16));
+                v[r][i].z += T::to_f32((u16)(w2[r][i].y & 0xffff));
+                v[r][i].w += T::to_f32((u16)(w2[r][i].y >> 16));
+            }
+            if constexpr (STORE_X) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
+        }
+        ln_row<V>(v[r], gm, bt, lane, (float)D);
+        store_row16<T, V>(h + (size_t)row * D, v[r], lane);
+    }
+}
+
+// rows per wave of add_layernorm_kernel (CLIPVIT_LN_RPW = 1 or 2, read at every launch).
+// Default 1: two rows per wave measured no faster in-model (LayerNorm family 0.447 -> 0.453
+// ms per forward at bs 256, tools/exp_lnrpw.sh) — one row per wave already streams at ~5.7 TB/s
+static int ln_rpw() {
+    const char* e = getenv("CLIPVIT_LN_RPW");
+    return e && atoi(e) == 2 ? 2 : 1;
 }
 
 #define DISPATCH_V(D, ...)                          \
@@ -242,6 +262,15 @@ void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsign
 
 void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
                           const float* b, int rows, int D) {
+    if (ln_rpw() == 2) {
+        dim3 grid((rows + 7) / 8), block(256);
+        if (dtype == 2) {
+            DISPATCH_V(D, add_layernorm_kernel<F16, V, true, false, 2><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
+        } else {
+            DISPATCH_V(D, add_layernorm_kernel<BF16, V, true, false, 2><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
+        }
+        return;
+    }
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
         DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
@@ -253,6 +282,12 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
 template <typename T, int V>
 static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
+    if (ln_rpw() == 2) {
+        dim3 grid((rows + 7) / 8), block(256);
+        if (y2) add_layernorm_kernel<T, V, true, true, 2><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 2><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
+        return;
+    }
     dim3 grid((rows + 3) / 4), block(256);
     if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
     else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
