@@ -1378,6 +1378,12 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         // 1.9 rounds of 256 CUs at 0.94x the work per tile, against 450 = 1.76 rounds of
         // 256x256 (whose second round is a full tile time). 98: 12 waves (3 x 4, 80 x 64 per
         // wave: three waves on every SIMD); 99: 6 waves (3 x 2, 80 x 128). LDS-staged epilogue.
+        // 256x192 tiles of 12 waves (4 x 3, 64 x 64 per wave: three waves on every SIMD) for
+        // the N = 768 roles: 4 N-tiles, 200 tiles at M = 12800 = one round on 200 CUs
+        case 89:
+            if (a.N % 192) return -1;
+            launch_pipe<T, 256, 192, 4, 3, 2, 3>(s, epi, a);
+            return 0;
         case 98:
             if (a.N % 256) return -1;
             launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);
