@@ -332,9 +332,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // [M1, M) on the role's small tile as a second launch. Row-wise independent outputs:
     // bit-identical to one launch. Measured (c_fc 12800 x 3072 x 768): 81.6 us in one launch
     // (128x128) or 77.6 (256x256, 3 rounds) -> 54.3 + 15.9 = 70.2 us.
+    // the main launch's tile: 256x256, or 256x192 for the 12-wave variants 69 / 89
+    const int bn = (h->split_main == 69 || h->split_main == 89) ? 192 : 256;
     if (h->round_split && !h->var_forced && (role == R_FC || role == R_QKV) && t256 &&
-        t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
-        const long nN = N / 256, R = t256 / h->ncu, rem = t256 % h->ncu;
+        N % bn == 0 && t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
+        const long nN = N / bn, tm = (long)((M + 255) / 256) * nN;
+        const long R = tm / h->ncu, rem = tm % h->ncu;
         const long m1 = R * h->ncu / nN * 256;
         if (R >= 1 && rem > 0 && 2 * rem <= h->ncu && m1 > 0 && m1 < M) {
             GemmArgs b = a;

@@ -1384,6 +1384,10 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 192) return -1;
             launch_pipe<T, 256, 192, 4, 3, 2, 3>(s, epi, a);
             return 0;
+        case 69:  // 89 with direct (unstaged) epilogue stores
+            if (a.N % 192) return -1;
+            launch_pipe<T, 256, 192, 4, 3, 2>(s, epi, a);
+            return 0;
         case 98:
             if (a.N % 256) return -1;
             launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);

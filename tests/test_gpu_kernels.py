@@ -30,10 +30,10 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 VARIANTS = list(range(1, 16)) + [21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 34, 40, 41, 42, 43,
                                   50, 51, 52, 53, 70, 71, 80, 81, 82, 208, 213, 221, 222, 230, 250, 251,
                                   252, 270, 280, 281, 282, 83, 84, 85, 283, 86, 87, 88, 90, 91,
-                                  413, 813, 1613, 1680, 422, 92, 93, 94, 95, 292, 293, 96, 97, 98, 99, 89]
+                                  413, 813, 1613, 1680, 422, 92, 93, 94, 95, 292, 293, 96, 97, 98, 99, 89, 69]
 N128 = (1, 2, 6, 7, 10, 11, 12, 13, 22, 26, 42, 43, 52, 81, 82, 87, 88)
 N256 = (3, 5, 8, 9, 14, 15, 21, 23, 24, 25, 27, 28, 29, 30, 31, 34, 40, 41, 50, 51, 53, 70, 71, 80, 83, 84, 85, 86, 98, 99)
-N192 = (92, 93, 94, 95, 89)
+N192 = (92, 93, 94, 95, 89, 69)
 STAGED = (80, 81, 82, 83, 85, 86, 88, 89, 92, 94, 98, 99)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
 PERSIST = (40, 41, 42, 43)  # persistent store-overlapped kernels (gemm_ps.hip)
 DEFER = (30, 31, 34)  # persistent deferred-epilogue kernels: 16-bit outputs, bias, K >= 640
