@@ -1044,9 +1044,10 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
-    // 16-bit-output kernels (variants 30-39 and 80-89, or epi 10 / 11 = 16-bit STORE / GELU on
-    // any variant): run, then widen to fp32
-    if ((variant >= 30 && variant < 40) || (variant >= 80 && variant < 90 && variant != 84 && variant != 87) || epi >= 10) {
+    // LDS-staged 16-bit-output variants (80-82, 98), or epi 10 / 11 = 16-bit STORE / GELU on
+    // any variant: run, then widen to fp32
+    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98;
+    if (staged || epi >= 10) {
         if (epi >= 10) epi -= 10;
         if (epi == 2) {
             hipFreeAsync(Wp, s);

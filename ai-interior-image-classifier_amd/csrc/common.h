@@ -12,43 +12,6 @@ typedef unsigned short u16;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
-// 16-byte global stores; NT = non-temporal (streamed past L2 so a GEMM's output does not
-// evict the operand panels the other tiles still re-read).
-template <bool NT>
-__device__ __forceinline__ void st16(void* p, uint4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)p);
-    else *(uint4*)p = v;
-}
-template <bool NT>
-__device__ __forceinline__ void st16f(void* p, float4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(f32x4v{v.x, v.y, v.z, v.w}, (f32x4v*)p);
-    else *(float4*)p = v;
-}
-
-// Output store policy of a GEMM epilogue: 0 plain, 1 non-temporal, 2 write-through (sc1:
-// the line leaves the XCD's L2 with the store, so the kernel ends with no dirty L2 lines that
-// the next kernel's reads on other XCDs would first have to wait for).
-template <int SM>
-struct OutStore {
-    __amdgpu_buffer_rsrc_t r;
-    unsigned char* base;
-    __device__ __forceinline__ explicit OutStore(void* C) : base((unsigned char*)C) {
-        if constexpr (SM == 2) r = __builtin_amdgcn_make_buffer_rsrc(C, 0, -1, 0x00020000);
-    }
-    __device__ __forceinline__ void u4(size_t off, uint4 v) {  // 16 B at byte offset off (< 4 GiB)
-        if constexpr (SM == 2)
-            __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, r, (int)off, 0, 16);
-        else if constexpr (SM == 1)
-            __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, (u32x4*)(base + off));
-        else
-            *(uint4*)(base + off) = v;
-    }
-    __device__ __forceinline__ void f4(size_t off, float4 v) {
-        u4(off, make_uint4(__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z),
-                           __float_as_uint(v.w)));
-    }
-};
-
 #define LDS_AS __attribute__((address_space(3)))
 #define GLB_AS __attribute__((address_space(1)))
 
@@ -134,7 +97,6 @@ enum Epi {
     EPI_PATCH = 3,   // C (f32) [remapped token row] = acc          (conv1 has no bias)
     EPI_F32 = 4,     // C (f32) = acc + bias                         (tests)
     EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
-    EPI_DISCARD = 6, // no stores (epilogue-cost ablation; timing only, pipelined kernel)
     EPI_GELU_Q8 = 7, // C (MX-fp8) = quickgelu(acc + bias), block scales to sC  (MX-fp8 GEMM)
     EPI_Q8 = 8,      // C (MX-fp8) = acc + bias, block scales to sC             (tests)
 };
@@ -237,12 +199,8 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
 }
 
 // ---- launchers (defined in the .hip translation units) ----
-// variant: 0 = auto by shape, 1 = 128x128 (4 waves), 2 = 256x128 (8 waves), 3 = 256x256 (8 waves)
+// variant: 0 = auto by shape; tile variants listed in gemm.hip launch_t
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
-// persistent store-overlapped variants 40-49 (gemm_ps.hip); ncu = compute units of the device
-int launch_gemm_ps(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant, int ncu);
-// deep-ring 256x256 variants 70-79 (gemm_deep.hip)
-int launch_gemm_deep(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
 
 // MX-fp8 path (mx8.hip). out16: 16-bit output type of EPI_STORE (1 bf16, 2 fp16).
 int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant);

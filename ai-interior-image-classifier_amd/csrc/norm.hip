@@ -217,13 +217,9 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
     }
 }
 
-// rows per wave of add_layernorm_kernel (CLIPVIT_LN_RPW = 1 or 2, read at every launch).
-// Default 1: two rows per wave measured no faster in-model (LayerNorm family 0.447 -> 0.453
-// ms per forward at bs 256, tools/exp_lnrpw.sh) — one row per wave already streams at ~5.7 TB/s
-static int ln_rpw() {
-    const char* e = getenv("CLIPVIT_LN_RPW");
-    return e && atoi(e) == 2 ? 2 : 1;
-}
+// add_layernorm_kernel runs one row per wave (RPW = 1): two rows per wave measured no faster
+// in-model in round 1 (LayerNorm family 0.447 -> 0.453 ms per forward at bs 256); one row per
+// wave already streams at ~5.7 TB/s.
 
 #define DISPATCH_V(D, ...)                          \
     switch ((D) / 256) {                            \
@@ -262,15 +258,6 @@ void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsign
 
 void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
                           const float* b, int rows, int D) {
-    if (ln_rpw() == 2) {
-        dim3 grid((rows + 7) / 8), block(256);
-        if (dtype == 2) {
-            DISPATCH_V(D, add_layernorm_kernel<F16, V, true, false, 2><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
-        } else {
-            DISPATCH_V(D, add_layernorm_kernel<BF16, V, true, false, 2><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
-        }
-        return;
-    }
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
         DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
@@ -282,12 +269,6 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
 template <typename T, int V>
 static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
-    if (ln_rpw() == 2) {
-        dim3 grid((rows + 7) / 8), block(256);
-        if (y2) add_layernorm_kernel<T, V, true, true, 2><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
-        else add_layernorm_kernel<T, V, false, false, 2><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
-        return;
-    }
     dim3 grid((rows + 3) / 4), block(256);
     if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
     else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);

@@ -3,7 +3,7 @@
 # counter group (rocprofv3 does not split counters over passes).
 set -o pipefail
 ROOT=$(pwd); OUT=$ROOT/gpurun_out/pmc; mkdir -p $OUT
-CASES=${CASES:-"12800,2304,768,0,208;12800,768,768,2,221;12800,3072,768,1,213;12800,768,3072,2,221"}
+CASES=${CASES:-"12800,2304,768,0,298;12800,768,768,0,282;12800,3072,768,1,213;12800,768,3072,0,282"}
 cd /tmp && export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 timeout -k 10 120 python3 $ROOT/tools/gemm_multi.py "$CASES" 20 > $OUT/timing.txt 2>&1 || exit 1
