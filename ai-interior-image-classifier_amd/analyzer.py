@@ -48,7 +48,7 @@ def synthetic_text_features(texts: list[str], dim: int) -> np.ndarray:
 class InteriorAnalyzer:
     def __init__(self, model: str | ViTConfig = "ViT-B/16", state_dict: dict | None = None,
                  use_lora: bool = False, lora_weights_path: str | None = None, lora_rank: int = 4,
-                 lora_alpha: float = 8, device: int | str = 0, compute_dtype: str = "bf16",
+                 lora_alpha: float = 8, device: int | str = 0, compute_dtype: str = "fp16",
                  dataset_json: str | Path = "interior_dataset.json",
                  text_features: dict[str, np.ndarray] | np.ndarray | None = None,
                  categories: dict[str, list[str]] | None = None, max_batch: int = 64,
@@ -170,6 +170,15 @@ class InteriorAnalyzer:
                 "reason": "Success - interior image analyzed"}
 
     # ------------------------------------------------------------------ public API
+    def logits(self, images, batch_size: int = 64) -> np.ndarray:
+        """The head's 100 * cos logits [n, C] of RGB PIL images (main.py:208 / 456 before the
+        softmax): detector columns first, then each analyzer segment (``self.table``)."""
+        rows = []
+        for a in range(0, len(images), batch_size):
+            out = self.engine.classify(self._pixels(images[a:a + batch_size]))
+            rows.append(out.logits.cpu().numpy())
+        return np.concatenate(rows, axis=0) if rows else np.zeros((0, self.engine.C), np.float32)
+
     def predict_batch(self, images, batch_size: int = 64, confidence_threshold: float = 0.3,
                       filter_interiors: bool = True) -> list[dict]:
         out = []

@@ -41,7 +41,7 @@ class ClassifyOutput:
 
 class VisionEngine:
     def __init__(self, cfg: ViTConfig, device: int | str | torch.device = 0,
-                 compute_dtype: str = "bf16", max_batch: int = 256):
+                 compute_dtype: str = "fp16", max_batch: int = 256):
         if not torch.cuda.is_available():
             raise _lib.ClipVitError(_lib.E_STATE, "no HIP device visible: the MI355X path needs a GPU")
         dev = torch.device(device if not isinstance(device, int) else f"cuda:{device}")

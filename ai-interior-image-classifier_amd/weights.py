@@ -9,6 +9,10 @@ Two sources:
 """
 from __future__ import annotations
 
+import collections
+import io
+import pickle
+import zipfile
 from pathlib import Path
 
 import numpy as np
@@ -103,25 +107,116 @@ def state_dict_checksum(sd: dict[str, torch.Tensor]) -> float:
     return float(sum(float(v.double().abs().sum()) for v in sd.values()))
 
 
+class _ScriptObject:
+    """Attribute bag standing in for a TorchScript class while an archive is read: the class's
+    code (the archive's ``code/`` entries) is never loaded or run."""
+
+    def __setstate__(self, state):
+        self.state = state
+
+
+_STORAGE_DTYPES = {"FloatStorage": torch.float32, "HalfStorage": torch.float16,
+                   "BFloat16Storage": torch.bfloat16, "DoubleStorage": torch.float64,
+                   "LongStorage": torch.int64, "IntStorage": torch.int32, "ShortStorage": torch.int16,
+                   "CharStorage": torch.int8, "ByteStorage": torch.uint8, "BoolStorage": torch.bool}
+
+
+class _StorageType:
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+
+def _rebuild_tensor(storage, offset, size, stride, *args):
+    return storage.as_strided(tuple(size), tuple(stride), offset)
+
+
+class _ArchiveUnpickler(pickle.Unpickler):
+    """Restricted unpickler for a torch zip archive's ``data.pkl``: rebuilds tensors from the
+    archive's raw storage records and turns every ``__torch__.*`` class into an inert
+    ``_ScriptObject``; any other global is refused (nothing from the file is executed)."""
+
+    def __init__(self, data: bytes, zf: zipfile.ZipFile, prefix: str):
+        super().__init__(io.BytesIO(data))
+        self.zf, self.prefix = zf, prefix
+
+    def find_class(self, module, name):
+        if module == "torch._utils" and name in ("_rebuild_tensor_v2", "_rebuild_tensor"):
+            return _rebuild_tensor
+        if module == "torch._utils" and name == "_rebuild_parameter":
+            return lambda data, requires_grad, hooks: data
+        if module == "collections" and name == "OrderedDict":
+            return collections.OrderedDict
+        if module == "torch" and name in _STORAGE_DTYPES:
+            return _StorageType(_STORAGE_DTYPES[name])
+        if module == "torch" and isinstance(getattr(torch, name, None), torch.dtype):
+            return getattr(torch, name)
+        if module.startswith("__torch__"):
+            return type(name, (_ScriptObject,), {})
+        raise pickle.UnpicklingError(f"refusing global {module}.{name} in a weights archive")
+
+    def persistent_load(self, pid):
+        kind, stype, key, _location, numel = pid[:5]
+        if kind != "storage":
+            raise pickle.UnpicklingError(f"unknown persistent record {kind!r}")
+        dtype = stype.dtype if isinstance(stype, _StorageType) else stype
+        raw = self.zf.read(f"{self.prefix}/data/{key}")
+        return torch.frombuffer(bytearray(raw), dtype=dtype)[:numel] if numel else torch.empty(0, dtype=dtype)
+
+
+def _flatten(obj, prefix: str, out: dict):
+    if isinstance(obj, torch.Tensor):
+        out[prefix[:-1]] = obj
+    elif isinstance(obj, _ScriptObject):
+        _flatten(getattr(obj, "state", None), prefix, out)
+    elif isinstance(obj, dict):
+        for k, v in obj.items():
+            if isinstance(k, str):
+                _flatten(v, prefix + k + ".", out)
+
+
+def is_torchscript_archive(path: str | Path) -> bool:
+    if not zipfile.is_zipfile(path):
+        return False
+    with zipfile.ZipFile(path) as zf:
+        return any(n.endswith("/constants.pkl") or "/code/" in n for n in zf.namelist())
+
+
+def read_torchscript_archive(path: str | Path) -> dict[str, torch.Tensor]:
+    """Tensors of a TorchScript archive (what clip.load downloads: ``ViT-*.pt``) by dotted
+    attribute path, e.g. ``visual.conv1.weight``, without executing anything from the file:
+    ``<root>/data.pkl`` is read by a restricted unpickler, the ``code/`` entries are ignored."""
+    with zipfile.ZipFile(path) as zf:
+        pkls = [n for n in zf.namelist() if n.endswith("/data.pkl") and n.count("/") == 1]
+        if not pkls:
+            raise ValueError(f"{path}: not a torch zip archive (no <root>/data.pkl)")
+        prefix = pkls[0].split("/")[0]
+        root = _ArchiveUnpickler(zf.read(pkls[0]), zf, prefix).load()
+        out: dict[str, torch.Tensor] = {}
+        _flatten(root, "", out)
+        return {k: v.clone() for k, v in out.items()}
+
+
 def load_openai_checkpoint(path: str | Path, text: bool = False) -> dict[str, torch.Tensor]:
     """Local OpenAI CLIP checkpoint -> fp32 ``visual.*`` state dict (``text=True``: the text
     tower's tensors instead, for TextEngine / InteriorAnalyzer(text_state_dict=...)).
 
-    Tries a plain state dict with ``torch.load(weights_only=True)`` first; an OpenAI
-    TorchScript archive (what clip.load downloads) is opened with ``torch.jit.load``, which
-    only a user-supplied file may be given to (nothing shipped in the reference is loaded).
+    A plain state dict is read with ``torch.load(weights_only=True)``; an OpenAI TorchScript
+    archive (what clip.load downloads; recognised by its ``constants.pkl`` / ``code/``
+    entries), which the weights-only loader refuses, is read by ``read_torchscript_archive`` —
+    neither path runs code from the file. Errors (missing file, corrupt archive, a pickle the
+    weights-only loader rejects) propagate unchanged.
     """
     path = Path(path)
-    try:
+    if is_torchscript_archive(path):
+        sd = read_torchscript_archive(path)
+    else:
         sd = torch.load(path, map_location="cpu", weights_only=True)
-        if hasattr(sd, "state_dict"):
-            sd = sd.state_dict()
-    except Exception:
-        sd = torch.jit.load(str(path), map_location="cpu").state_dict()
+        if not isinstance(sd, dict):
+            raise ValueError(f"{path}: expected a state dict, got {type(sd).__name__}")
     keep = (lambda k: not k.startswith("visual.") and k not in ("logit_scale", "input_resolution",
                                                                  "context_length", "vocab_size")) \
         if text else (lambda k: k.startswith("visual."))
-    return {k: v.float().contiguous() for k, v in sd.items() if keep(k)}
+    return {k: v.float().contiguous() for k, v in sd.items() if keep(k) and isinstance(v, torch.Tensor)}
 
 
 def as_host_f32(t) -> np.ndarray:

@@ -57,7 +57,7 @@ def parse():
                         "mxfp8 = BASELINE config 5 (MX-fp8 Linears, bf16 attention; bar 2e-2 vs bf16)")
     p.add_argument("--lora-rank", type=int, default=8)
     p.add_argument("--inflight", type=int, default=1, help="batches in flight on separate HIP streams")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=16.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--profile-iters", type=int, default=5)
     p.add_argument("--share-gpu", action="store_true",
@@ -65,42 +65,88 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(cfg, seconds: float):
-    """The oracle (CPU fp32 restatement, 'port') on the host cores: bs=16 (reference default,
-    main.py:592) batches of the same synthetic inputs until ~`seconds` of work."""
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_leg(name: str, batch: int, seconds: float):
+    """images/s of the oracle (encode + head) on `batch`-image batches for ~`seconds`."""
     from oracle import clip_ref
-    threads = min(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)), os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    cfg = C.get_config(name)
     sd = synthetic_state_dict(cfg, 0)
     geo = clip_ref.GEOMETRIES[cfg.name]
     g = torch.Generator().manual_seed(0)
-    px = torch.randn(16, 3, cfg.image_size, cfg.image_size, generator=g).clamp_(-1.8, 2.2)
+    px = torch.randn(batch, 3, cfg.image_size, cfg.image_size, generator=g).clamp_(-1.8, 2.2)
     T = torch.nn.functional.normalize(torch.randn(N_CLASSES, cfg.embed_dim, generator=g), dim=-1)
     with torch.no_grad():
-        clip_ref.head(clip_ref.encode_image(sd, geo, px[:2]), T, SEGMENTS)  # warm-up
+        clip_ref.head(clip_ref.encode_image(sd, geo, px[:1]), T, SEGMENTS)  # warm-up
         n, t0 = 0, time.perf_counter()
         while True:
             clip_ref.head(clip_ref.encode_image(sd, geo, px), T, SEGMENTS)
-            n += px.shape[0]
+            n += batch
             el = time.perf_counter() - t0
-            if el >= seconds and n >= 32:
+            if el >= seconds and n >= 2 * batch:
                 break
-    return {"value": round(n / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} synthetic {cfg.image_size}px images, bs=16, {cfg.name} fp32 torch-CPU oracle "
-                      f"(encode + head), {el:.1f}s"}
+    return {"model": name, "batch": batch, "value": round(n / el, 3), "images": n, "seconds": round(el, 2)}
+
+
+def cpu_baseline(cfg, seconds: float):
+    """The oracle (CPU fp32 torch restatement of the same forward + head, 'port') on ALL host
+    cores, BASELINE.md §4's legs: ViT-B/32 (the metric's model) and ViT-B/16 (the model the
+    reference runs, main.py:152 / 241) at bs=1 (the detector's batch, main.py:201) and bs=16
+    (the analyzer default, main.py:592). `value` = the metric model's bs=16 leg."""
+    threads = os.cpu_count() or 1
+    torch.set_num_threads(threads)
+    per = seconds / 4
+    legs = [_cpu_leg(m, b, per) for m in (cfg.name, "ViT-B/16" if cfg.name != "ViT-B/16" else "ViT-B/32")
+            for b in (1, 16)]
+    main = legs[1]
+    return {"value": main["value"], "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(),
+            "sample": f"{main['images']} synthetic {cfg.image_size}px images, bs=16, {cfg.name} fp32 "
+                      f"torch-CPU oracle (encode + head), {main['seconds']}s; legs: " +
+                      ", ".join(f"{l['model']} bs={l['batch']}: {l['value']} img/s" for l in legs),
+            "legs": legs}
+
+
+def parity_check(eng, px, T, cfg, n: int = 4):
+    """Max relative logit error of the engine against the CPU fp32 oracle on the first n images
+    of the benched batch (same weights, LoRA merged), per image max|dlogit| / max|logit_ref|."""
+    import numpy as np
+    from oracle import clip_ref
+    sd = synthetic_state_dict(cfg, 0)
+    for ad in (synthetic_adapters(cfg, rank=eng._lora_rank) if eng._lora_rank else []):
+        sd[ad.target] = clip_ref.merge_lora(sd[ad.target], torch.from_numpy(ad.A), torch.from_numpy(ad.B), ad.scaling)
+    x = px[:n].float().cpu()
+    with torch.no_grad():
+        f = clip_ref.encode_image(sd, clip_ref.GEOMETRIES[cfg.name], x)
+        _, lr, _, _, _ = clip_ref.head(f, T, SEGMENTS)
+    lg = eng.classify(px[:n]).logits.cpu().numpy()
+    lr = lr.numpy()
+    return float((np.abs(lg - lr).max(axis=1) / np.abs(lr).max(axis=1)).max())
 
 
 def load_traffic(cfg_name: str, batch: int):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC passes of this bench
+    command (tools/profile_round.sh -> profiles/pmc_traffic.json, which records the round it was
+    measured in): (bytes, source) or (None, None)."""
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
-        return None
+        return None, None
     try:
         d = json.loads(f.read_text())
         e = d.get(f"{cfg_name}|{batch}")
-        return None if e is None else e.get("mlp_gemm_bytes_per_launch")
-    except Exception:
-        return None
+        if e is None:
+            return None, None
+        return e.get("mlp_gemm_bytes_per_launch"), e.get("source", "profiles/pmc_traffic.json")
+    except (OSError, ValueError):
+        return None, None
 
 
 def main():
@@ -121,6 +167,7 @@ def main():
 
     eng = VisionEngine(cfg, dev, a.dtype, max_batch=a.batch)
     eng.load_state_dict(synthetic_state_dict(cfg, 0))
+    eng._lora_rank = a.lora_rank
     if a.lora_rank:
         eng.load_lora(synthetic_adapters(cfg, rank=a.lora_rank))
     g = torch.Generator().manual_seed(1234)
@@ -165,6 +212,8 @@ def main():
         el = float(t.item())
     imgs = world * a.batch * a.steps
     value = imgs / el
+    # --share-gpu: N ranks on ONE device (gloo) -- a code-path rehearsal, never a scaling point
+    n_gpus = 1 if a.share_gpu else world
 
     # live per-kernel-family device times (HIP events on the launch stream)
     fam = eng.profile_forward(px, iters=a.profile_iters)
@@ -181,11 +230,13 @@ def main():
     gflop_img = cfg.gflop_per_image() - pruned
     model_tflops = value / world * gflop_img / 1e3
 
+    traffic, traffic_src = load_traffic(cfg.name, a.batch)
     line = {
         "metric": "images/sec @ 224x224 bs=256, ViT-B/32+LoRA, 1/2/4/8 MI355X; % MFMA roofline",
         "value": round(value, 2),
         "unit": "images/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
+        "ranks": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(el / a.steps * 1e3, 4),
@@ -196,17 +247,25 @@ def main():
         "data": "synthetic (seeded N(0,1) pixels clamped to CLIP-normalised range, seeded CLIP-style weights, synthetic unit text features)",
         "config": {"workload": f"{cfg.name} + merged LoRA r={a.lora_rank} classify (encode_image + cosine head over {N_CLASSES} labels, 6 segments)",
                    "image_size": cfg.image_size, "per_gpu_batch": a.batch, "global_batch": a.batch * world,
-                   "parallelism": f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else ""),
+                   "parallelism": (f"dp{world} rehearsal on one GPU, gloo all-gather (not a scaling point)"
+                                   if a.share_gpu else f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else "")),
                    "batches_in_flight": a.inflight},
         "roofline": {"bound": "mfma", "kernel": "mlp GEMMs (c_fc+QuickGELU, c_proj)",
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": load_traffic(cfg.name, a.batch),
+                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(mlp_ms, 5),
                      "model_mfma_frac": round(model_tflops / peak, 4),
                      "gflop_per_image_executed": round(gflop_img, 4),
                      "family_ms_per_forward": {k: round(v, 4) for k, v in fam.items()}},
         "cpu_baseline": None,
     }
+    if rank == 0 and a.lora_rank is not None:
+        bar = 2e-2 if a.dtype == "mxfp8" else 1e-3
+        err = parity_check(eng, px, T, cfg)
+        line["parity"] = {"max_rel_logit_err_vs_cpu_fp32_oracle": round(err, 6), "images": 4, "bar": bar,
+                          "meets_bar": err <= bar,
+                          "note": "per image max|dlogit|/max|logit_ref| on the benched batch's first images"
+                                  + ("; mxfp8's bar is 2e-2 against the bf16 engine" if a.dtype == "mxfp8" else "")}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)
     if rank == 0:

@@ -16,16 +16,18 @@ main.py:93-109 suffix-matches ``named_parameters`` against the checkpoint keys):
     transformer.resblocks.i.*  (text tower, width 512, 8 heads), token_embedding,
     positional_embedding, ln_final, text_projection, logit_scale
 
-The text tower here is a stand-in: the BPE tokenizer and real text weights are absent
-offline, so ``tokenize`` keeps the prompt strings and ``encode_text`` embeds each string by
-a crc32-seeded token embedding, then runs the (LoRA-wrapped) text transformer with CLIP's
-causal mask, ln_final and text_projection of the last position. Text features are therefore
-synthetic but deterministic and LoRA-dependent, like the reference's.
+The text tower is OpenAI's ``encode_text`` [3p] with real token ids: ``token_embedding`` of the
+ids + ``positional_embedding`` -> the (LoRA-wrapped) causal transformer -> ``ln_final`` -> the
+row at each prompt's end-of-text id (``text.argmax(-1)``) @ ``text_projection``. The OpenAI BPE
+vocabulary file is absent offline, so ``tokenize`` is CLIP's ``tokenize`` (sot + ids + eot, zero
+padding to 77) over a merges list learned from the reference's own prompt vocabulary
+(tests/golden/bpe_merges.txt), with HF ``tokenizers`` (transformers' CLIPTokenizer) doing the
+byte-level BPE — an implementation independent of the product's ``tokenizer.py``. Text weights
+are seeded synthetic tensors with the OpenAI names.
 """
 from __future__ import annotations
 
 import types
-import zlib
 from collections import OrderedDict
 
 import torch
@@ -104,13 +106,14 @@ class VisionTransformer(nn.Module):
 
 
 class CLIPMirror(nn.Module):
-    def __init__(self, geo: Geometry, text_width=512, text_layers=12, text_heads=8, context=77):
+    def __init__(self, geo: Geometry, vocab: int, text_width=512, text_layers=12, text_heads=8,
+                 context=77):
         super().__init__()
         self.context_length = context
         self.visual = VisionTransformer(geo)
         mask = torch.full((context, context), float("-inf")).triu_(1)
         self.transformer = Transformer(text_width, text_layers, text_heads, attn_mask=mask)
-        self.token_embedding = nn.Embedding(1, text_width)        # stand-in (no BPE vocab)
+        self.token_embedding = nn.Embedding(vocab, text_width)
         self.positional_embedding = nn.Parameter(torch.zeros(context, text_width))
         self.ln_final = LayerNorm(text_width)
         self.text_projection = nn.Parameter(torch.zeros(text_width, geo.embed_dim))
@@ -124,68 +127,83 @@ class CLIPMirror(nn.Module):
         return self.visual(image.type(self.dtype))
 
     def encode_text(self, text):
-        strings = text.strings if hasattr(text, "strings") else list(text)
-        width = self.positional_embedding.shape[1]
-        emb = []
-        for s in strings:
-            g = torch.Generator().manual_seed(zlib.crc32(s.encode("utf-8")))
-            emb.append(torch.randn(self.context_length, width, generator=g) * 0.02)
-        x = torch.stack(emb).to(self.dtype) + self.positional_embedding.to(self.dtype)
+        x = self.token_embedding(text).type(self.dtype)
+        x = x + self.positional_embedding.type(self.dtype)
         x = self.transformer(x.permute(1, 0, 2)).permute(1, 0, 2)
-        x = self.ln_final(x)
-        return x[:, -1, :] @ self.text_projection
+        x = self.ln_final(x).type(self.dtype)
+        return x[torch.arange(x.shape[0]), text.argmax(dim=-1)] @ self.text_projection
 
 
-def init_text_tower(model: CLIPMirror, seed: int = 1234):
-    """Deterministic CLIP-style init of the stand-in text tower (not part of any fixture)."""
-    g = torch.Generator().manual_seed(seed)
-    with torch.no_grad():
-        for name, p in model.named_parameters():
-            if name.startswith("visual."):
-                continue
-            if p.ndim >= 2:
-                p.copy_(torch.randn(p.shape, generator=g) * 0.02)
-            elif name.endswith("weight") and ("ln_" in name):
-                p.fill_(1.0)
-            elif name != "logit_scale":
-                p.zero_()
-
-
-def load_visual(model: CLIPMirror, sd: dict):
-    """Copy ``visual.*`` tensors (OpenAI names) into the mirror."""
+def load_params(model: CLIPMirror, sd: dict):
+    """Copy OpenAI-named tensors (``visual.*`` and text-tower names) into the mirror."""
     own = dict(model.named_parameters())
     with torch.no_grad():
         for k, v in sd.items():
-            if k.startswith("visual."):
+            if k in own:
                 own[k].copy_(torch.as_tensor(v, dtype=torch.float32).reshape(own[k].shape))
 
 
-class _Tokens:
-    def __init__(self, strings):
-        self.strings = list(strings)
+def clip_vocab(merges):
+    """CLIP's vocabulary construction [3p simple_tokenizer]: 256 byte symbols, the same with
+    ``</w>``, one entry per merge, then <|startoftext|>, <|endoftext|>."""
+    bs = list(range(ord("!"), ord("~") + 1)) + list(range(ord("¡"), ord("¬") + 1)) + \
+        list(range(ord("®"), ord("ÿ") + 1))
+    cs, n = bs[:], 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    syms = [chr(c) for c in cs]
+    vocab = syms + [s + "</w>" for s in syms] + ["".join(m) for m in merges]
+    vocab += ["<|startoftext|>", "<|endoftext|>"]
+    return {v: i for i, v in enumerate(vocab)}
 
-    def to(self, device):
-        return self
+
+def read_merges_file(path):
+    lines = open(path, encoding="utf-8").read().split("\n")[1:]
+    return [tuple(l.split()) for l in lines if l.strip()]
 
 
-def make_clip_shim(visual_sd_by_name: dict, text_seed: int = 1234):
+def make_tokenize(merges):
+    """``clip.tokenize`` over ``merges`` with HF tokenizers' byte-level BPE (CLIPTokenizer)."""
+    from transformers import CLIPTokenizer
+    hf = CLIPTokenizer(vocab=clip_vocab(merges), merges=[tuple(m) for m in merges])
+
+    def tokenize(texts, context_length=77, truncate=False):
+        texts = [texts] if isinstance(texts, str) else list(texts)
+        out = torch.zeros(len(texts), context_length, dtype=torch.long)
+        for i, t in enumerate(texts):
+            ids = hf(t)["input_ids"]
+            if len(ids) > context_length:
+                if not truncate:
+                    raise RuntimeError(f"Input {t} is too long for context length {context_length}")
+                ids = ids[:context_length]
+                ids[-1] = hf.eos_token_id
+            out[i, :len(ids)] = torch.tensor(ids)
+        return out
+
+    return tokenize
+
+
+def make_clip_shim(sd_by_name: dict, merges):
     """A module object usable as ``sys.modules['clip']`` for the reference's harness.
 
-    ``load(name, device)`` returns (CLIPMirror with the seeded visual weights registered for
-    ``name``, preprocess) exactly as main.py:152 / main.py:241 expect.
+    ``load(name, device)`` returns (CLIPMirror carrying the seeded weights registered for
+    ``name`` — ``visual.*`` and the text tower —, preprocess) exactly as main.py:152 /
+    main.py:241 expect; ``tokenize`` is clip.tokenize over ``merges``.
     """
     shim = types.ModuleType("clip")
+    vocab = len(merges) + 514
 
     def load(name, device="cpu", **kw):
         geo = GEOMETRIES[name]
-        m = CLIPMirror(geo)
-        init_text_tower(m, text_seed)
-        load_visual(m, visual_sd_by_name[name])
+        m = CLIPMirror(geo, vocab)
+        load_params(m, sd_by_name[name])
         m.eval()
         return m, (lambda img: preprocess(img, geo.image_size))
 
     shim.load = load
     shim.base_load = load
-    shim.tokenize = lambda texts, context_length=77, truncate=False: _Tokens(
-        [texts] if isinstance(texts, str) else texts)
+    shim.tokenize = make_tokenize(merges)
     return shim

@@ -3,17 +3,25 @@
 Runs only in the build container (it imports /root/reference/main.py, which never travels to
 the GPU box). The real ``clip`` package and weights are absent offline, so ``sys.modules['clip']``
 is the oracle's OpenAI-CLIP module mirror (oracle/clip_module.py) carrying seeded synthetic
-weights; everything AFTER ``clip.load`` is the reference's code, unmodified:
+weights (vision tower AND text tower, OpenAI names) and a ``clip.tokenize`` over a BPE merges
+list learned from the reference's own prompt vocabulary; everything AFTER ``clip.load`` /
+``clip.tokenize`` is the reference's code, unmodified:
 
   * LoRA binding facts: main.py ``replace_linears_with_lora`` + ``load_lora_weights_to_model``
     (main.py:62-113) on the mirror with the shipped ``lora_models/comprehensive_lora*.pth``
     -> lora_binding.json (counts, missing names, vision delta, dead out_proj delta).
-  * Harness outputs: main.py ``CachedInteriorAnalyzer`` (use_lora=True, the shipped checkpoint,
-    CPU) + ``InteriorImageDetector`` on interior_sample.jpg and four dataset images, with
-    PYTHONHASHSEED=0 (the label order depends on it) -> harness_<model>.json
-    (result dicts, label order) + harness_<model>.npz (text matrices, oracle logits).
-  * Copies the input JPEGs and interior_dataset.json (data files the reference reads at run
-    time) into tests/golden/ so the GPU-box tests need nothing from /root/reference.
+  * Harness outputs, for BOTH models (ViT-B/32, ViT-B/16) x BOTH shipped checkpoints: main.py
+    ``CachedInteriorAnalyzer(use_lora=True, <checkpoint>)`` + ``InteriorImageDetector`` on
+    interior_sample.jpg and ALL 150 dataset images (75 of them larger than 256 px, up to
+    2592x1944: the downscale path; interior87.jpg is the image listed twice with conflicting
+    labels in interior_dataset.json), PYTHONHASHSEED=0 (label order)
+    -> harness_<model>_<ckpt>.json (result dicts of analyze_images_batch with and without the
+    interior filter, is_interior_image per image, label order) + harness_<model>_<ckpt>.npz
+    (the harness's 100*cos logits [151, 40 + C] and pixel checksums) + text_<ckpt>.npz (the
+    detector's and the analyzer's cached text matrices).
+  * Copies the input JPEGs, interior_dataset.json and the two LoRA checkpoints (data files the
+    reference reads at run time) into tests/golden/ so the GPU-box tests need nothing from
+    /root/reference; writes the learned merges to bpe_merges.txt.
 
     python tests/golden/make_golden.py            # re-executes itself with PYTHONHASHSEED=0
 """
@@ -24,16 +32,21 @@ import os
 import shutil
 import subprocess
 import sys
-import types
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
 ROOT = HERE.parents[1]
 REF = Path("/root/reference")
-IMAGES = ["interior_sample.jpg", "dataset_images/interior5.jpg", "dataset_images/interior6.jpg",
-          "dataset_images/interior7.jpg", "dataset_images/interior8.jpg"]
+IMAGES = ["interior_sample.jpg"] + [f"dataset_images/interior{i}.jpg" for i in range(1, 151)]
 MODELS = ["ViT-B/32", "ViT-B/16"]
+CKPTS = ["comprehensive_lora.pth", "comprehensive_lora_new.pth"]
 WEIGHT_SEED = 0
+TEXT_SEED = 1
+N_MERGES = 600
+
+
+def tag_of(model, ckpt):
+    return model.replace("/", "").replace("-", "").lower() + "_" + ckpt.replace("comprehensive_", "").replace(".pth", "")
 
 
 def _setup():
@@ -41,15 +54,32 @@ def _setup():
     import amd_pkg
     amd_pkg.load()
     import torch
-    from interior_amd.config import get_config
-    from interior_amd.weights import synthetic_state_dict, state_dict_checksum
-    from oracle.clip_module import make_clip_shim
-    sds = {m: synthetic_state_dict(get_config(m), WEIGHT_SEED) for m in MODELS}
-    shim = make_clip_shim(sds)
+    from interior_amd import labels as L
+    from interior_amd import tokenizer as TK
+    from interior_amd.config import TextConfig, get_config
+    from interior_amd.weights import state_dict_checksum, synthetic_state_dict, synthetic_text_state_dict
+    from oracle.clip_module import make_clip_shim, read_merges_file
+    # merges learned from the reference's own prompts (detector + analyzer label prompts)
+    cats = L.extract_categories(L.load_training_data(REF / "interior_dataset.json"))
+    corpus = L.build_label_table(cats).all_texts
+    merges = TK.learn_merges(corpus, N_MERGES)
+    (HERE / "bpe_merges.txt").write_text("#version: learned from the reference's label prompts (tests/golden/make_golden.py)\n"
+                                        + "\n".join(" ".join(m) for m in merges) + "\n", encoding="utf-8")
+    merges = read_merges_file(HERE / "bpe_merges.txt")
+    tc = TextConfig(vocab=514 + len(merges))
+    text_sd = synthetic_text_state_dict(tc, TEXT_SEED)
+    sds = {m: {**synthetic_state_dict(get_config(m), WEIGHT_SEED), **text_sd} for m in MODELS}
+    shim = make_clip_shim(sds, merges)
+    # the oracle's tokenize (HF tokenizers) and the product tokenizer agree on every prompt
+    mine = TK.SimpleTokenizer(bpe_path=HERE / "bpe_merges.txt")
+    assert (shim.tokenize(corpus).numpy() == mine.tokenize(corpus)).all()
     sys.modules["clip"] = shim
     sys.path.insert(0, str(REF))
     import main as ref_main  # the reference harness
-    return torch, ref_main, shim, sds, state_dict_checksum
+    checks = {"weights": {m: {"seed": WEIGHT_SEED, "checksum": state_dict_checksum(synthetic_state_dict(get_config(m), WEIGHT_SEED))}
+                          for m in MODELS},
+              "text_weights": {"seed": TEXT_SEED, "vocab": tc.vocab, "checksum": state_dict_checksum(text_sd)}}
+    return torch, ref_main, shim, checks
 
 
 def lora_facts(torch, ref_main, shim, ckpt_name):
@@ -65,7 +95,6 @@ def lora_facts(torch, ref_main, shim, ckpt_name):
         for i in range(12):
             model.visual.transformer.resblocks[i].attn.out_proj.lora.lora_B.fill_(1.0)
         dead = model.encode_image(px)
-        txt_before = None
     ckpt = torch.load(REF / "lora_models" / ckpt_name, map_location="cpu", weights_only=True)
     return {
         "checkpoint": ckpt_name,
@@ -81,16 +110,14 @@ def lora_facts(torch, ref_main, shim, ckpt_name):
     }
 
 
-def harness(torch, ref_main, shim, model_name):
-    import numpy as np
+def harness(torch, ref_main, shim, model_name, ckpt):
     from PIL import Image
     base_load = shim.base_load  # every clip.load(...) of the harness gets `model_name` weights
     ref_main.clip.load = lambda name, device="cpu", **kw: base_load(model_name, device)
     cwd = os.getcwd()
     os.chdir(REF)  # main.py:264 reads interior_dataset.json relative to the CWD
     try:
-        an = ref_main.CachedInteriorAnalyzer(use_lora=True,
-                                             lora_weights_path="lora_models/comprehensive_lora.pth",
+        an = ref_main.CachedInteriorAnalyzer(use_lora=True, lora_weights_path=f"lora_models/{ckpt}",
                                              lora_rank=4, lora_alpha=8, device="cpu")
         paths = [str(REF / p) for p in IMAGES]
         with torch.no_grad():
@@ -99,18 +126,19 @@ def harness(torch, ref_main, shim, model_name):
             res_nf = an.analyze_images_batch(paths, batch_size=16, filter_interiors=False)
             det = [list(an.detector.is_interior_image(Image.open(p).convert("RGB"), 0.3)) for p in paths]
             pix = torch.stack([an.preprocess(Image.open(p).convert("RGB")) for p in paths])
-            f = an.model.encode_image(pix)
+            f = torch.cat([an.model.encode_image(pix[a:a + 16]) for a in range(0, len(paths), 16)])
             f = f / f.norm(dim=-1, keepdim=True)
             T = {c: t.float().numpy() for c, t in an.text_features_cache.items()}
             T_det = an.detector.text_features.float().numpy()
-            logits = {c: (100.0 * f @ torch.from_numpy(t).t()).numpy() for c, t in T.items()}
-            logits["detector"] = (100.0 * f @ torch.from_numpy(T_det).t()).numpy()
+            logits = 100.0 * f @ torch.cat([torch.from_numpy(T_det)] + [torch.from_numpy(T[c]) for c in T]).t()
     finally:
         os.chdir(cwd)
     key = lambda p: Path(p).name
     out = {
         "model": model_name,
+        "checkpoint": ckpt,
         "weights_seed": WEIGHT_SEED,
+        "text_seed": TEXT_SEED,
         "pythonhashseed": os.environ.get("PYTHONHASHSEED"),
         "images": [Path(p).name for p in IMAGES],
         "categories": an.all_categories,
@@ -122,11 +150,11 @@ def harness(torch, ref_main, shim, model_name):
     }
     flat = pix.reshape(len(IMAGES), -1)
     idx = torch.arange(0, flat.shape[1], 151)  # 997 fixed sample positions per image
-    arrays = {"T_det": T_det, **{f"T_{c}": t for c, t in T.items()},
-              **{f"logits_{c}": v for c, v in logits.items()},
+    arrays = {"logits": logits.numpy(),
               "pixels_sum": flat.double().sum(1).numpy(), "pixels_abs_sum": flat.double().abs().sum(1).numpy(),
               "pixels_sample": flat[:, idx].numpy(), "pixels_sample_idx": idx.numpy()}
-    return out, arrays
+    text = {"T_det": T_det, **{f"T_{c}": t for c, t in T.items()}}
+    return out, arrays, text
 
 
 def main():
@@ -134,21 +162,24 @@ def main():
         env = dict(os.environ, PYTHONHASHSEED="0")
         sys.exit(subprocess.call([sys.executable, __file__], env=env))
     import numpy as np
-    torch, ref_main, shim, sds, checksum = _setup()
+    torch, ref_main, shim, checks = _setup()
     (HERE / "images").mkdir(exist_ok=True)
+    (HERE / "lora").mkdir(exist_ok=True)
     for p in IMAGES:
         shutil.copyfile(REF / p, HERE / "images" / Path(p).name)
+    for c in CKPTS:
+        shutil.copyfile(REF / "lora_models" / c, HERE / "lora" / c)
     shutil.copyfile(REF / "interior_dataset.json", HERE / "interior_dataset.json")
-    facts = {"weights": {m: {"seed": WEIGHT_SEED, "checksum": checksum(sds[m])} for m in MODELS},
-             "checkpoints": [lora_facts(torch, ref_main, shim, c)
-                             for c in ("comprehensive_lora.pth", "comprehensive_lora_new.pth")]}
+    facts = {**checks, "checkpoints": [lora_facts(torch, ref_main, shim, c) for c in CKPTS]}
     (HERE / "lora_binding.json").write_text(json.dumps(facts, indent=1, ensure_ascii=False))
-    for m in MODELS:
-        out, arrays = harness(torch, ref_main, shim, m)
-        tag = m.replace("/", "").replace("-", "").lower()
-        (HERE / f"harness_{tag}.json").write_text(json.dumps(out, indent=1, ensure_ascii=False))
-        np.savez_compressed(HERE / f"harness_{tag}.npz", **arrays)
-        print("wrote", tag)
+    for c in CKPTS:
+        for m in MODELS:
+            out, arrays, text = harness(torch, ref_main, shim, m, c)
+            tag = tag_of(m, c)
+            (HERE / f"harness_{tag}.json").write_text(json.dumps(out, ensure_ascii=False))
+            np.savez_compressed(HERE / f"harness_{tag}.npz", **arrays)
+            np.savez_compressed(HERE / f"text_{c.replace('comprehensive_', '').replace('.pth', '')}.npz", **text)
+            print("wrote", tag, flush=True)
 
 
 if __name__ == "__main__":

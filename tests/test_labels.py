@@ -5,7 +5,7 @@ from interior_amd import labels as L
 
 
 def test_categories_equal_reference_sets(golden_dir):
-    js = json.loads((golden_dir / "harness_vitb32.json").read_text())
+    js = json.loads((golden_dir / "harness_vitb32_lora.json").read_text())
     mine = L.extract_categories(L.load_training_data(golden_dir / "interior_dataset.json"))
     ref = js["categories"]  # reference order under PYTHONHASHSEED=0 (set order)
     assert {k: len(v) for k, v in mine.items()} == {"styles": 20, "characteristics": 299,
@@ -15,7 +15,7 @@ def test_categories_equal_reference_sets(golden_dir):
 
 
 def test_detector_categories_match_reference(golden_dir):
-    js = json.loads((golden_dir / "harness_vitb32.json").read_text())
+    js = json.loads((golden_dir / "harness_vitb32_lora.json").read_text())
     assert L.DETECTOR_CATEGORIES == js["detector_categories"]
     assert L.N_INTERIOR == 11
 
