@@ -4,7 +4,7 @@
 // load time, keeps the text-feature table, and runs the encoder forward as a fixed sequence of
 // hand-written gfx950 kernels on the caller's stream:
 //
-//   im2col -> GEMM(patch, EPI_PATCH) -> embed+ln_pre+ln_1
+//   implicit-GEMM patch embedding (pixels -> LDS patch tiles, EPI_PATCH) -> embed+ln_pre+ln_1
 //   12x [ GEMM(qkv) -> attention -> GEMM(out_proj, +residual) -> ln_2
 //         -> GEMM(c_fc, QuickGELU) -> GEMM(c_proj, +residual) -> ln_1(next) ]
 //   -> ln_post(CLS) @ proj -> [classify: L2-norm, 100*cos logits, segment softmax, top-5]
@@ -70,7 +70,7 @@ struct Lane {
     float* x = nullptr;  // [cap*N, D] fp32 residual stream
     void* h = nullptr;   // [cap*N, D] 16-bit LN output; also the attention output
     void* qkv = nullptr; // [cap*N, 3D]
-    void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the im2col buffer
+    void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the 16-bit pixel copy of a cast input
     float* f = nullptr;  // [cap, E] projected features
     unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
     hipStream_t stream = nullptr;
@@ -232,7 +232,9 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
     for (auto& l : w->lane) {
         l.cap = lane_cap(h);
         const size_t rows = (size_t)l.cap * h->N;
-        const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)l.cap * h->G2 * h->Kp * 2);
+        const size_t R = h->cfg.image_size;
+        const size_t Rw = (R / h->cfg.patch_size) * ((h->cfg.patch_size + 7) / 8 * 8);  // padded pixel rows
+        const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)l.cap * 3 * R * Rw * 2);
         if (e == hipSuccess) e = hipMalloc(&l.x, rows * h->D * sizeof(float));
         if (e == hipSuccess) e = hipMalloc(&l.h, rows * h->D * 2);
         if (e == hipSuccess) e = hipMalloc(&l.qkv, rows * 3 * h->D * 2);
@@ -367,6 +369,32 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     return 0;
 }
 
+// conv1 as an implicit GEMM over the pixels (gemm.hip PIMPL): 16-bit pixels of the compute type
+// feed the patch tiles directly; other input dtypes are cast once into the u buffer.
+static int patch_embed(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B, Lane* w) {
+    const int R = h->cfg.image_size, P = h->cfg.patch_size;
+    const void* px16 = pix;
+    int Rw = R;
+    if (P % 8) {  // P = 14: patch rows padded to 16 pixels (aligned 16-byte chunks)
+        Rw = (R / P) * 16;
+        launch_cast_pixels_padded(s, in_dtype, h->dt, pix, w->u, B, R, P);
+        px16 = w->u;
+    } else if (in_dtype != h->dt) {
+        launch_cast_pixels(s, in_dtype, h->dt, pix, w->u, (size_t)B * 3 * R * R);
+        px16 = w->u;
+    }
+    GemmArgs a{};
+    a.A = px16; a.W = h->wpatch; a.bias = nullptr; a.C = w->x;
+    a.M = B * h->G2; a.N = h->D; a.K = h->Kp; a.ldc = h->D;
+    a.patch_g2 = h->G2; a.patch_ntok = h->N; a.patch_R = R; a.patch_Rw = Rw;
+    a.xcd_n = h->xcd[R_PATCH];
+    if (launch_patch_gemm(s, h->dt, P, a) != 0) {
+        g_err = "patch embedding: unsupported patch size / width";
+        return CLIPVIT_E_INVALID;
+    }
+    return 0;
+}
+
 // MX-fp8 GEMM: A = (A8, A8 + M*K scales), W = packed (N*K e4m3 bytes, then scales).
 static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char* A8,
                  const void* Wq, const float* bias, void* C, int M, int N, int K, int ldc,
@@ -447,9 +475,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         else launch_layernorm(s, h->dt, w->x, w->h, g, b, M, D);
     };
     if (prof) prof->mark(s, F_EMBED);
-    launch_im2col(s, in_dtype, h->dt, pix, w->u, B, h->cfg.image_size, h->cfg.patch_size, h->Kp);
-    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, R_PATCH);
-    if (rc) return rc;
+    if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
     if (h->q8_layer(0))
         launch_embed_ln_q8(s, w->x, q8, q8s, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
@@ -506,9 +532,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     const int D = h->D, N = h->N, M = B * N;
     int rc;
     if (prof) prof->mark(s, F_EMBED);
-    launch_im2col(s, in_dtype, h->dt, pix, w->u, B, h->cfg.image_size, h->cfg.patch_size, h->Kp);
-    rc = gemm(s, h, EPI_PATCH, w->u, h->wpatch, nullptr, w->x, B * h->G2, D, h->Kp, D, R_PATCH);
-    if (rc) return rc;
+    if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
                     B, N, D);
@@ -651,8 +675,9 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     g_err.clear();
     if (!cfg || !out) FAIL(CLIPVIT_E_INVALID, "null argument");
     const clipvit_config& c = *cfg;
-    if (c.patch_size <= 0 || c.image_size % c.patch_size)
-        FAIL(CLIPVIT_E_INVALID, "image_size must be a multiple of patch_size");
+    if (c.patch_size != 14 && c.patch_size != 16 && c.patch_size != 32)
+        FAIL(CLIPVIT_E_INVALID, "patch_size must be 14, 16 or 32");
+    if (c.image_size % c.patch_size) FAIL(CLIPVIT_E_INVALID, "image_size must be a multiple of patch_size");
     if (c.width % 256 || c.width < 512 || c.width > 1280)
         FAIL(CLIPVIT_E_INVALID, "width must be a multiple of 256 in [512, 1280]");
     if (c.heads * 64 != c.width) FAIL(CLIPVIT_E_INVALID, "heads * 64 must equal width");
@@ -673,7 +698,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->N = h->G2 + 1;
     h->D = c.width;
     h->E = c.embed_dim;
-    h->K3 = 3 * c.patch_size * c.patch_size;
+    // patch length in the implicit patch GEMM's k order (row length padded to a multiple of 8)
+    h->K3 = 3 * c.patch_size * ((c.patch_size + 7) / 8 * 8);
     h->Kp = (h->K3 + 63) / 64 * 64;
     h->mx8 = c.compute_dtype == CLIPVIT_MXFP8;
     h->dt = h->mx8 ? CLIPVIT_BF16 : c.compute_dtype;  // 16-bit type of everything not MX-fp8
@@ -782,7 +808,7 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     };
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
-    size_t maxw = D * h->Kp;
+    size_t maxw = D * h->K3;
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         HIPCHK(alloc16(ly.wqkv, 3 * D * D));
@@ -805,7 +831,8 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
         h->scratch_elems = maxw;
     }
     hipStream_t s = nullptr;
-    pack_linear(h, s, "visual.conv1.weight", h->wpatch, nullptr);
+    launch_patch_weight_relayout(s, h->master["visual.conv1.weight"], h->scratch, (int)D, h->cfg.patch_size);
+    launch_pack_weight(s, h->dt, h->scratch, h->wpatch, (int)D, h->K3, h->Kp);
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         pack_linear(h, s, L(i, "attn.in_proj_weight"), ly.wqkv, nullptr);

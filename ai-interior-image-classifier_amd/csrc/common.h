@@ -108,6 +108,7 @@ struct GemmArgs {
     void* C;           // output, row stride ldc (elements)
     int M, N, K, ldc;
     int patch_g2, patch_ntok;  // EPI_PATCH row remap: m -> (m / g2) * ntok + 1 + m % g2
+    int patch_R, patch_Rw;     // implicit patch GEMM: image side R, pixel row length Rw (A = [B, 3, R, Rw])
     int xcd_n;  // tile->XCD partition: 2 = 4 M-bands x 2 N-halves per XCD group (else 1-D)
     // MX-fp8 GEMM only: E8M0 block scales [rows][K/32] of A and W, [M][N/32] of a Q8 output
     const unsigned char* sA;
@@ -201,6 +202,15 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape; tile variants listed in gemm.hip launch_t
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
+// implicit-GEMM patch embedding (no im2col): P = patch size (14, 16, 32), a.A = pixels
+int launch_patch_gemm(hipStream_t s, int dtype, int P, const GemmArgs& a);
+// pixels of any supported dtype -> 16-bit pixels of the compute type (same [B, 3, R, R] layout)
+void launch_cast_pixels(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, size_t n);
+// [B, 3, R, R] -> [B, 3, R, G * 16] 16-bit with every P-pixel patch row padded to 16 (zeros)
+void launch_cast_pixels_padded(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B,
+                               int R, int P);
+// conv1.weight [D, 3, P, P] fp32 -> [D, 3 * P * roundup8(P)] in the implicit patch GEMM's k order
+void launch_patch_weight_relayout(hipStream_t s, const float* w, float* out, int D, int P);
 
 // MX-fp8 path (mx8.hip). out16: 16-bit output type of EPI_STORE (1 bf16, 2 fp16).
 int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant);
@@ -227,8 +237,6 @@ void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal = false);
 
-void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, void* acol, int B,
-                   int R, int P, int Kp);
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
                      const float* b1, int B, int N, int D);

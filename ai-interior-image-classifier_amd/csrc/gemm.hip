@@ -188,8 +188,25 @@ __device__ __forceinline__ void wait_tile(int r) {
     vm_wait<0>();
 }
 
+// Implicit-GEMM patch embedding (PIMPL = patch size P > 0): the A operand is the 16-bit NCHW
+// pixel tensor itself. Row m of A = patch (image b, py, px); the patch's k order is
+// k = c * (P * PP) + r * PP + j (PP = P rounded up to a multiple of 8), so every 8-element
+// (16-byte) LDS chunk is 8 consecutive pixels of ONE pixel row. Pixel rows hold G * PP pixels
+// (a.patch_Rw): for P = 14 the input is first copied with every 14-pixel patch row padded to 16
+// (launch_cast_pixels_padded; the packed conv weight is zero at j = 14, 15), for P = 16 / 32 the
+// pixels are used as given. Each staging piece is a global_load_lds from
+// pix + patch_base(m) + patch_koff(k): the patch tile goes straight from the image into LDS,
+// with no im2col buffer.
+template <int P>
+__device__ __forceinline__ int patch_koff(int kq, int R, int Rw) {
+    constexpr int PP = (P + 7) / 8 * 8, CH = P * PP;
+    if (kq >= 3 * CH) return 0;  // K padding: any in-bounds address (the weights there are zero)
+    const int c = kq / CH, rem = kq - c * CH, r = rem / PP, j0 = rem - r * PP;
+    return (c * R + r) * Rw + j0;
+}
+
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
@@ -221,11 +238,21 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     const int mlast = a.M - 1;
     // per-thread source row offsets (constant over k)
     size_t asrc[LA], wsrc[LW];
+    int acol[LA];  // PIMPL: the piece's (swizzled) 16-B chunk inside the 64-wide k-tile
 #pragma unroll
     for (int r = 0; r < LA; ++r) {
         const int p = r * NT * 16 + tid * 16;
         const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
-        asrc[r] = (size_t)min(m0 + row, mlast) * ldb + c * 16;
+        if constexpr (PIMPL > 0) {
+            constexpr int PP = (PIMPL + 7) / 8 * 8;
+            const int m = min(m0 + row, mlast), R = a.patch_R, Rw = a.patch_Rw, G = R / PIMPL;
+            const int b = m / a.patch_g2, pp = m - b * a.patch_g2, py = pp / G, px = pp - py * G;
+            asrc[r] = ((size_t)b * 3 * R * Rw + (size_t)py * PIMPL * Rw + px * PP) * 2;
+            acol[r] = c;
+        } else {
+            asrc[r] = (size_t)min(m0 + row, mlast) * ldb + c * 16;
+            acol[r] = 0;
+        }
     }
 #pragma unroll
     for (int r = 0; r < LW; ++r) {
@@ -239,8 +266,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         const size_t kofs = (size_t)kt * 128;
 #pragma unroll
         for (int r = 0; r < LA; ++r)
-            if (r * NT * 16 + wave * 1024 < A_BYTES)  // wave-uniform
-                glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
+            if (r * NT * 16 + wave * 1024 < A_BYTES) {  // wave-uniform
+                if constexpr (PIMPL > 0)
+                    glds16(Ab + asrc[r] + 2 * (size_t)patch_koff<PIMPL>(kt * 64 + 8 * acol[r], a.patch_R, a.patch_Rw),
+                           sA + r * NT * 16 + wave * 1024);
+                else
+                    glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
+            }
 #pragma unroll
         for (int r = 0; r < LW; ++r)
             if (r * NT * 16 + wave * 1024 < W_BYTES)
@@ -450,6 +482,24 @@ static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
         case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
         case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
     }
+}
+
+// Implicit-GEMM patch embedding on 160x128 tiles (4 waves, two workgroups per CU: the v22 tile
+// of the im2col path); a.A = 16-bit pixels [B, 3, R, Rw], a.K = padded patch length,
+// a.patch_R = R, a.patch_Rw = pixel row length (R, or G * 16 for P = 14).
+template <typename T>
+static int launch_patch_t(hipStream_t s, int P, const GemmArgs& a) {
+    if (a.N % 128) return -1;
+    const int nwg = grid_for((a.M + 159) / 160, a.N / 128, a.xcd_n);
+    switch (P) {
+        case 14: gemm_pipe_kernel<T, 160, 128, 2, 2, 2, EPI_PATCH, 0, 14><<<nwg, 256, 0, s>>>(a); return 0;
+        case 16: gemm_pipe_kernel<T, 160, 128, 2, 2, 2, EPI_PATCH, 0, 16><<<nwg, 256, 0, s>>>(a); return 0;
+        case 32: gemm_pipe_kernel<T, 160, 128, 2, 2, 2, EPI_PATCH, 0, 32><<<nwg, 256, 0, s>>>(a); return 0;
+    }
+    return -1;
+}
+int launch_patch_gemm(hipStream_t s, int dtype, int P, const GemmArgs& a) {
+    return dtype == 2 ? launch_patch_t<F16>(s, P, a) : launch_patch_t<BF16>(s, P, a);
 }
 
 // 16-bit -> fp32 copy (test entry for the 16-bit-output kernels)

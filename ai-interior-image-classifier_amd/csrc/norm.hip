@@ -1,9 +1,9 @@
-// Memory-bound kernels of the encoder: patch im2col, token assembly + ln_pre + ln_1,
+// Memory-bound kernels of the encoder: pixel cast, token assembly + ln_pre + ln_1,
 // LayerNorm, weight packing and the load-time LoRA merge.
 //
 // Reference semantics (OpenAI-CLIP VisionTransformer.forward [3p], called via
 // model.encode_image at main.py:204 / 444 / 503):
-//   x = conv1(pixels)                         (no bias; -> im2col + MFMA GEMM, EPI_PATCH)
+//   x = conv1(pixels)                         (no bias; implicit MFMA GEMM on the pixels, EPI_PATCH)
 //   x = cat([class_embedding, x]) + positional_embedding
 //   x = ln_pre(x)                             (CLIP LayerNorm: computed in fp32, eps 1e-5)
 //   per block: x = x + attn(ln_1(x)); x = x + mlp(ln_2(x))
@@ -13,9 +13,10 @@
 namespace clipvit {
 
 // ---------------------------------------------------------------------------------------
-// im2col of non-overlapping p x p patches: acol[b*G*G + py*G + px][c*p*p + i*p + j]
-//   = pix[b][c][py*p + i][px*p + j], columns >= 3*p*p zero-padded up to Kp (multiple of 64).
-// One thread writes 8 consecutive columns (one 16-byte store).
+// Pixel cast for the implicit-GEMM patch embedding (gemm.hip, PIMPL): the patch GEMM reads
+// 16-bit NCHW pixels of the compute type straight into LDS; pixels given in fp32 (or the other
+// 16-bit type) are converted once, 8 per thread (CLIP's encode_image casts its input to the
+// model dtype the same way: image.type(self.dtype) [3p]).
 template <int IN>
 __device__ __forceinline__ float load_pix(const void* p, size_t off) {
     if constexpr (IN == 0) return ((const float*)p)[off];
@@ -24,67 +25,90 @@ __device__ __forceinline__ float load_pix(const void* p, size_t off) {
 }
 
 template <typename TO, int IN>
-__global__ void im2col_kernel(const void* __restrict__ pix, u16* __restrict__ acol, int B, int R,
-                              int P, int Kp) {
-    const int G = R / P, G2 = G * G, K3 = 3 * P * P;
-    const long total = (long)B * G2 * (Kp / 8);
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int kc = (int)(idx % (Kp / 8));
-    const long row = idx / (Kp / 8);
-    const int b = (int)(row / G2), pp = (int)(row % G2);
-    const int py = pp / G, px = pp % G;
+__global__ void cast_pixels_kernel(const void* __restrict__ src, u16* __restrict__ dst, size_t n8) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
     float v[8];
-    const int k0 = kc * 8;
-    if (k0 + 8 <= K3 && (P % 8) == 0) {
-        // 8 consecutive columns = 8 consecutive pixels of one patch row
-        const int c = k0 / (P * P), rem = k0 % (P * P), i = rem / P, jj = rem % P;
-        const size_t off = (((size_t)b * 3 + c) * R + (py * P + i)) * R + px * P + jj;
-        if constexpr (IN == 0) {
-            const float4* src = (const float4*)((const float*)pix + off);
-            const float4 a0 = src[0], a1 = src[1];
-            v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
-            v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
-        } else {
-            const uint4 w = *(const uint4*)((const u16*)pix + off);
-            const u16* hv = (const u16*)&w;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                v[e] = IN == 1 ? BF16::to_f32(hv[e]) : F16::to_f32(hv[e]);
-        }
+    if constexpr (IN == 0) {
+        const float4* s = (const float4*)src + 2 * i;
+        const float4 a0 = s[0], a1 = s[1];
+        v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
+        v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
     } else {
+        const uint4 w = ((const uint4*)src)[i];
+        const u16* hv = (const u16*)&w;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = k0 + e;
-            float val = 0.f;
-            if (k < K3) {
-                const int c = k / (P * P), rem = k % (P * P), i = rem / P, jj = rem % P;
-                val = load_pix<IN>(pix, (((size_t)b * 3 + c) * R + (py * P + i)) * R + px * P + jj);
-            }
-            v[e] = val;
-        }
+        for (int e = 0; e < 8; ++e) v[e] = IN == 1 ? BF16::to_f32(hv[e]) : F16::to_f32(hv[e]);
     }
-    uint4 o = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                         pack2<TO>(v[6], v[7]));
-    *(uint4*)(acol + row * Kp + k0) = o;
+    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                  pack2<TO>(v[6], v[7]));
 }
 
 template <typename TO>
-static void im2col_dispatch(hipStream_t s, int in_dtype, const void* pix, void* acol, int B, int R,
-                            int P, int Kp) {
-    const int G = R / P;
-    const long total = (long)B * G * G * (Kp / 8);
-    const int threads = 256;
-    const long blocks = (total + threads - 1) / threads;
-    if (in_dtype == 0) im2col_kernel<TO, 0><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
-    else if (in_dtype == 1) im2col_kernel<TO, 1><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
-    else im2col_kernel<TO, 2><<<blocks, threads, 0, s>>>(pix, (u16*)acol, B, R, P, Kp);
+static void cast_dispatch(hipStream_t s, int in_dtype, const void* src, void* dst, size_t n) {
+    const size_t n8 = n / 8;  // n = B * 3 * R * R, R a multiple of 14 or 16 -> 3 R^2 % 8 == 0 for even R
+    const unsigned g = (unsigned)((n8 + 255) / 256);
+    if (in_dtype == 0) cast_pixels_kernel<TO, 0><<<g, 256, 0, s>>>(src, (u16*)dst, n8);
+    else if (in_dtype == 1) cast_pixels_kernel<TO, 1><<<g, 256, 0, s>>>(src, (u16*)dst, n8);
+    else cast_pixels_kernel<TO, 2><<<g, 256, 0, s>>>(src, (u16*)dst, n8);
 }
 
-void launch_im2col(hipStream_t s, int in_dtype, int out_dtype, const void* pix, void* acol, int B,
-                   int R, int P, int Kp) {
-    if (out_dtype == 2) im2col_dispatch<F16>(s, in_dtype, pix, acol, B, R, P, Kp);
-    else im2col_dispatch<BF16>(s, in_dtype, pix, acol, B, R, P, Kp);
+// conv1.weight [D, 3, P, P] -> [D, 3 * P * PP] in the implicit patch GEMM's k order (gemm.hip
+// patch_koff): k = c * P * PP + r * PP + j, zero for the row padding j >= P. For P a multiple of
+// 8 this is the identity layout.
+__global__ void patch_weight_relayout_kernel(const float* __restrict__ w, float* __restrict__ out, int D,
+                                             int P, int PP) {
+    const int K = 3 * P * PP;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long)D * K) return;
+    const int n = (int)(i / K), k = (int)(i % K);
+    const int c = k / (P * PP), rem = k % (P * PP), r = rem / PP, j = rem % PP;
+    out[i] = j < P ? w[(((size_t)n * 3 + c) * P + r) * P + j] : 0.f;
+}
+
+// [B, 3, R, R] (any pixel dtype) -> [B, 3, R, G * 16] of the 16-bit compute type, every P-pixel
+// patch row followed by 16 - P zeros (P = 14: the implicit patch GEMM then reads each patch row
+// as two aligned 16-byte chunks). One thread per 8 output pixels.
+template <typename TO, int IN>
+__global__ void cast_pixels_padded_kernel(const void* __restrict__ src, u16* __restrict__ dst, int B, int R,
+                                          int P) {
+    const int G = R / P, Rw = G * 16;
+    const long n8 = (long)B * 3 * R * Rw / 8;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const long row = i / (Rw / 8);                 // (b * 3 + c) * R + y
+    const int x0 = (int)(i % (Rw / 8)) * 8, px = x0 >> 4, j0 = x0 & 15;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int j = j0 + e;
+        v[e] = j < P ? load_pix<IN>(src, (size_t)row * R + px * P + j) : 0.f;
+    }
+    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                  pack2<TO>(v[6], v[7]));
+}
+
+void launch_cast_pixels_padded(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B,
+                               int R, int P) {
+    const long n8 = (long)B * 3 * R * (R / P) * 16 / 8;
+    const unsigned g = (unsigned)((n8 + 255) / 256);
+#define CPP(TO, IN) cast_pixels_padded_kernel<TO, IN><<<g, 256, 0, s>>>(src, (u16*)dst, B, R, P)
+    if (out_dtype == 2) {
+        if (in_dtype == 0) CPP(F16, 0); else if (in_dtype == 1) CPP(F16, 1); else CPP(F16, 2);
+    } else {
+        if (in_dtype == 0) CPP(BF16, 0); else if (in_dtype == 1) CPP(BF16, 1); else CPP(BF16, 2);
+    }
+#undef CPP
+}
+void launch_patch_weight_relayout(hipStream_t s, const float* w, float* out, int D, int P) {
+    const int PP = (P + 7) / 8 * 8;
+    const long n = (long)D * 3 * P * PP;
+    patch_weight_relayout_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(w, out, D, P, PP);
+}
+
+void launch_cast_pixels(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, size_t n) {
+    if (out_dtype == 2) cast_dispatch<F16>(s, in_dtype, src, dst, n);
+    else cast_dispatch<BF16>(s, in_dtype, src, dst, n);
 }
 
 // ---------------------------------------------------------------------------------------

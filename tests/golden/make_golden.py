@@ -17,7 +17,8 @@ list learned from the reference's own prompt vocabulary; everything AFTER ``clip
     labels in interior_dataset.json), PYTHONHASHSEED=0 (label order)
     -> harness_<model>_<ckpt>.json (result dicts of analyze_images_batch with and without the
     interior filter, is_interior_image per image, label order) + harness_<model>_<ckpt>.npz
-    (the harness's 100*cos logits [151, 40 + C] and pixel checksums) + text_<ckpt>.npz (the
+    (the harness's 100*cos logits [151, 40 + C], its L2-normalised image features and pixel
+    checksums) + text_<ckpt>.npz (the
     detector's and the analyzer's cached text matrices).
   * Copies the input JPEGs, interior_dataset.json and the two LoRA checkpoints (data files the
     reference reads at run time) into tests/golden/ so the GPU-box tests need nothing from
@@ -150,7 +151,7 @@ def harness(torch, ref_main, shim, model_name, ckpt):
     }
     flat = pix.reshape(len(IMAGES), -1)
     idx = torch.arange(0, flat.shape[1], 151)  # 997 fixed sample positions per image
-    arrays = {"logits": logits.numpy(),
+    arrays = {"logits": logits.numpy(), "features": f.numpy(),
               "pixels_sum": flat.double().sum(1).numpy(), "pixels_abs_sum": flat.double().abs().sum(1).numpy(),
               "pixels_sample": flat[:, idx].numpy(), "pixels_sample_idx": idx.numpy()}
     text = {"T_det": T_det, **{f"T_{c}": t for c, t in T.items()}}

@@ -93,7 +93,7 @@ def test_main_py_call_sequence_on_the_facade(gpu, golden_dir):
             ref = ref_logits[:32, off:off + lg.shape[1]]
             off += lg.shape[1]
             err = np.abs(lg - ref).max(axis=1) / np.abs(ref_logits[:32]).max(axis=1)
-            assert err.max() < 2e-3, (category, float(err.max()))
+            assert err.max() < 3e-3, (category, float(err.max()))  # fp16 text tower adds ~1.5e-3
     model.close()
     clip.set_tokenizer(None)
 
