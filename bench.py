@@ -93,6 +93,7 @@ def _cpu_leg(name: str, batch: int, seconds: float):
             el = time.perf_counter() - t0
             if el >= seconds and n >= 2 * batch:
                 break
+    print(f"[bench] cpu leg {name} bs={batch}: {n / el:.2f} img/s", file=sys.stderr, flush=True)
     return {"model": name, "batch": batch, "value": round(n / el, 3), "images": n, "seconds": round(el, 2)}
 
 
@@ -101,7 +102,10 @@ def cpu_baseline(cfg, seconds: float):
     cores, BASELINE.md §4's legs: ViT-B/32 (the metric's model) and ViT-B/16 (the model the
     reference runs, main.py:152 / 241) at bs=1 (the detector's batch, main.py:201) and bs=16
     (the analyzer default, main.py:592). `value` = the metric model's bs=16 leg."""
-    threads = os.cpu_count() or 1
+    # the box's own CPU share: the affinity mask / OMP_NUM_THREADS (os.cpu_count() reports the
+    # whole machine there, and oversubscribing it stalls the run)
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", avail)), avail))
     torch.set_num_threads(threads)
     per = seconds / 4
     legs = [_cpu_leg(m, b, per) for m in (cfg.name, "ViT-B/16" if cfg.name != "ViT-B/16" else "ViT-B/32")
@@ -215,6 +219,7 @@ def main():
     # --share-gpu: N ranks on ONE device (gloo) -- a code-path rehearsal, never a scaling point
     n_gpus = 1 if a.share_gpu else world
 
+    print(f"[bench] timed {a.steps} steps: {value:.1f} img/s", file=sys.stderr, flush=True)
     # live per-kernel-family device times (HIP events on the launch stream)
     fam = eng.profile_forward(px, iters=a.profile_iters)
     lane_b = int(fam.pop("lane_batch"))  # images per launch (per stream lane)

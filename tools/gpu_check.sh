@@ -1,11 +1,14 @@
 #!/bin/bash
 # One GPU call: GPU tests, default bench, then (arg "prof") the rocprof passes of
-# tools/profile_round.sh. Every GPU step has its own time limit; the first failure ends the call.
+# tools/profile_round.sh. Every GPU step has its own time limit; the first failure ends the call
+# (a test failure included: nothing else runs on the GPU after a failed or timed-out step).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-  > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -3 gpurun_out/gpu_tests.log
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
-tail -2 gpurun_out/bench.log
-if [ "$1" = "prof" ]; then bash tools/profile_round.sh gpurun_out/prof && echo prof-ok; fi
+if [ "$1" != "nontest" ]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -v -s --timeout 200 --timeout-method thread \
+    > gpurun_out/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
+  tail -3 gpurun_out/gpu_tests.log
+fi
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.log
+if [ "$1" = "prof" ] || [ "$2" = "prof" ]; then bash tools/profile_round.sh gpurun_out/prof && echo prof-ok; fi
