@@ -62,6 +62,8 @@ struct DeviceGuard {
 struct LayerW {
     void *wqkv = nullptr, *wout = nullptr, *wfc = nullptr, *wproj = nullptr;
     const float *bqkv, *bout, *bfc, *bproj, *ln1g, *ln1b, *ln2g, *ln2b;
+    // LayerNorm fold (lnfold): ln_1 into QKV, ln_2 into c_fc: s_n = sum_k W'_nk, b' = b + W beta
+    float *s_qkv = nullptr, *bf_qkv = nullptr, *s_fc = nullptr, *bf_fc = nullptr;
 };
 
 // One lane = the activation buffers for `cap` images + the HIP stream that runs them.
@@ -72,6 +74,7 @@ struct Lane {
     void* qkv = nullptr; // [cap*N, 3D]
     void* u = nullptr;   // [cap*N, 4D] MLP hidden; also the 16-bit pixel copy of a cast input
     float* f = nullptr;  // [cap, E] projected features
+    float2* st = nullptr;  // lnfold: [cap*N, D/128] per-row 128-column (mean, M2) of x
     unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
@@ -163,6 +166,11 @@ struct clipvit_handle {
     bool resid16 = false;
     // deferred residual store (fp16 path, see forward()); CLIPVIT_DEFER_X=0 disables
     bool defer_x = true;
+    // LayerNorm fold (fp16 default; CLIPVIT_LNFOLD=0 disables): ln_1 / ln_2
+    // become per-row statistics written by the residual producers' epilogues (out_proj, c_proj,
+    // embedding) and an affine correction in the QKV / c_fc epilogues; no LayerNorm pass
+    bool lnfold = false;
+    float* scratch2 = nullptr;  // W diag(gamma) staging for the folded Linears
     // last block on class-token rows only (see cls_tail); CLIPVIT_CLS_PRUNE=0 disables
     bool cls_prune = true;
     unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
@@ -212,6 +220,7 @@ static int free_ws(Workspace* w) {
         hipFree(l.qkv);
         hipFree(l.u);
         hipFree(l.f);
+        hipFree(l.st);
         hipFree(l.q8);
         if (l.done) hipEventDestroy(l.done);
         if (l.stream) hipStreamDestroy(l.stream);
@@ -240,6 +249,7 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess) e = hipMalloc(&l.qkv, rows * 3 * h->D * 2);
         if (e == hipSuccess) e = hipMalloc(&l.u, ubytes);
         if (e == hipSuccess) e = hipMalloc((void**)&l.f, (size_t)l.cap * h->E * sizeof(float));
+        if (e == hipSuccess && h->lnfold) e = hipMalloc((void**)&l.st, rows * (h->D / 128) * sizeof(float2));
         if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
@@ -313,11 +323,21 @@ static void release_ws(clipvit_handle* h, Workspace* w) {
 
 enum Role { R_QKV = 0, R_OUT, R_FC, R_PROJ, R_PATCH };
 
+// LayerNorm-fold operands of a GEMM (EPI_LNF*, EPI_RES_STATS; GemmArgs)
+struct Fold {
+    const float* s = nullptr;
+    const float2* st_in = nullptr;
+    float2* st_out = nullptr;
+    void* C2 = nullptr;
+    int np = 0;
+};
+
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
-                const float* bias, void* C, int M, int N, int K, int ldc, int role) {
+                const float* bias, void* C, int M, int N, int K, int ldc, int role, const Fold& fo = Fold()) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
+    a.lnf_s = fo.s; a.st_in = fo.st_in; a.st_out = fo.st_out; a.C2 = fo.C2; a.np = fo.np;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
     int variant = h->var[role];
@@ -337,7 +357,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the main launch's tile: 256x256, or 256x192 for the 12-wave variants 69 / 89
     const int bn = (h->split_main == 69 || h->split_main == 89) ? 192 : 256;
     if (h->round_split && !h->var_forced && (role == R_FC || role == R_QKV) && t256 &&
-        N % bn == 0 && t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
+        N % bn == 0 && t256 < 4L * h->ncu &&
+        (epi == EPI_STORE || epi == EPI_GELU || epi == EPI_LNF || epi == EPI_LNF_GELU)) {
         const long nN = N / bn, tm = (long)((M + 255) / 256) * nN;
         const long R = tm / h->ncu, rem = tm % h->ncu;
         const long m1 = R * h->ncu / nN * 256;
@@ -348,6 +369,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             GemmArgs c = a;
             c.A = (const unsigned char*)A + (size_t)m1 * K * 2;
             c.C = (unsigned char*)C + (size_t)m1 * ldc * 2;
+            if (c.st_in) c.st_in += (size_t)m1 * c.np;
             c.M = M - (int)m1;
             c.xcd_n = 0;
             if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 &&
@@ -524,11 +546,105 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
     return 0;
 }
 
+// Class-token tail of the last block on the LayerNorm-fold path (see cls_tail): the gathered
+// CLS rows go through the same per-row arithmetic as the full block — out_proj on the full-M
+// out_proj tile (160x128, EPI_RES_STATS: x += ., x16, the 128-column statistics in the same
+// order), c_fc with the folded ln_2, c_proj (+x, fp32) — so the features equal the unpruned
+// forward's bit for bit; then ln_post @ proj.
+static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof) {
+    const int D = h->D, N = h->N, np = D / 128;
+    const LayerW& ly = h->layers[h->cfg.layers - 1];
+    unsigned char* base = (unsigned char*)w->u;
+    float* xc = (float*)base;
+    u16* hc = (u16*)(base + (size_t)B * D * 4);
+    u16* yc = hc + (size_t)B * D;
+    u16* uc = yc + (size_t)B * D;
+    float2* sc = (float2*)(uc + (size_t)B * 4 * D);
+    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D);
+    auto g0 = [&](int epi, int variant, const void* A, const void* W, const float* bias, void* C, int n, int k,
+                  const Fold& fo) {
+        GemmArgs a{};
+        a.A = A; a.W = W; a.bias = bias; a.C = C;
+        a.M = B; a.N = n; a.K = k; a.ldc = n;
+        a.lnf_s = fo.s; a.st_in = fo.st_in; a.st_out = fo.st_out; a.C2 = fo.C2; a.np = fo.np;
+        if (launch_gemm(s, h->dt, epi, a, variant) != 0) {
+            g_err = "cls tail gemm: unsupported shape";
+            return CLIPVIT_E_INVALID;
+        }
+        return 0;
+    };
+    int rc;
+    Fold fo;
+    fo.st_out = sc; fo.C2 = yc; fo.np = np;
+    if ((rc = g0(EPI_RES_STATS, 82, hc, ly.wout, ly.bout, xc, D, D, fo))) return rc;
+    if (prof) prof->mark(s, F_TAIL);
+    Fold f2;
+    f2.s = ly.s_fc; f2.st_in = sc; f2.np = np;
+    if ((rc = g0(EPI_LNF_GELU, h->tail_var, yc, ly.wfc, ly.bf_fc, uc, 4 * D, D, f2))) return rc;
+    if (prof) prof->mark(s, F_TAIL);
+    if ((rc = g0(EPI_RESID, h->tail_var, uc, ly.wproj, ly.bproj, xc, D, 4 * D, Fold()))) return rc;
+    if (prof) prof->mark(s, F_TAIL);
+    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E);
+    if (prof) prof->mark(s, F_HEAD);
+    return 0;
+}
+
+// Encoder forward with the LayerNorm fold. Buffers: x fp32 residual;
+// x16 = 16-bit copy of x (the A operand of QKV in h, of c_fc in the dead qkv buffer); st = the
+// per-row 128-column statistics of x. Per block:
+//   QKV   = EPI_LNF(x16 (h), W_qkv diag(ln_1.g))        -> qkv        [ln_1 folded]
+//   attn  (qkv)                                          -> h
+//   out   = EPI_RES_STATS(h, W_out): x += ., x16 -> qkv[0, M*D), st
+//   c_fc  = EPI_LNF_GELU(x16 (qkv), W_fc diag(ln_2.g))  -> u          [ln_2 folded]
+//   c_proj= EPI_RES_STATS(u, W_proj): x += ., x16 -> h, st
+static int forward_fold(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B, Lane* w,
+                        float* f_out, Prof* prof) {
+    const int D = h->D, N = h->N, M = B * N, np = D / 128;
+    int rc;
+    if (prof) prof->mark(s, F_EMBED);
+    if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
+    launch_embed_stats(s, h->dt, w->x, w->h, w->st, h->cls, h->pos, h->lnpre_g, h->lnpre_b, B, N, D);
+    if (prof) prof->mark(s, F_EMBED);
+    void* x16b = w->qkv;  // x16 after out_proj (qkv is dead once attention has read it)
+    const int nl = h->cfg.layers;
+    for (int i = 0; i < nl; ++i) {
+        const LayerW& ly = h->layers[i];
+        Fold fq;
+        fq.s = ly.s_qkv; fq.st_in = w->st; fq.np = np;
+        if ((rc = gemm(s, h, EPI_LNF, w->h, ly.wqkv, ly.bf_qkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, fq))) return rc;
+        if (prof) prof->mark(s, F_QKV);
+        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        if (prof) prof->mark(s, F_ATTN);
+        if (i + 1 == nl && h->cls_prune) {
+            if ((rc = cls_tail_fold(h, s, B, w, f_out, prof))) return rc;
+            HIPCHK(hipGetLastError());
+            return 0;
+        }
+        Fold fo;
+        fo.st_out = w->st; fo.C2 = x16b; fo.np = np;
+        if ((rc = gemm(s, h, EPI_RES_STATS, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT, fo))) return rc;
+        if (prof) prof->mark(s, F_OUT);
+        Fold ff;
+        ff.s = ly.s_fc; ff.st_in = w->st; ff.np = np;
+        if ((rc = gemm(s, h, EPI_LNF_GELU, x16b, ly.wfc, ly.bf_fc, w->u, M, 4 * D, D, 4 * D, R_FC, ff))) return rc;
+        if (prof) prof->mark(s, F_FC);
+        Fold fp;
+        fp.st_out = w->st; fp.C2 = w->h; fp.np = np;
+        if ((rc = gemm(s, h, EPI_RES_STATS, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ, fp))) return rc;
+        if (prof) prof->mark(s, F_PROJ);
+    }
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    if (prof) prof->mark(s, F_HEAD);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Encoder forward for B images on stream s with lane buffers w; writes the projected
 // (un-normalised) features to f_out.
 static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
                    Lane* w, float* f_out, Prof* prof) {
     if (h->mx8) return forward_mx8(h, s, pix, in_dtype, B, w, f_out, prof);
+    if (h->lnfold) return forward_fold(h, s, pix, in_dtype, B, w, f_out, prof);
     const int D = h->D, N = h->N, M = B * N;
     int rc;
     if (prof) prof->mark(s, F_EMBED);
@@ -662,6 +778,21 @@ static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name
         launch_pack_weight_mx8(s, w, q, q + (size_t)N * K, N, K, K);
         return 0;
     }
+    // LayerNorm fold: in_proj carries ln_1, c_fc carries ln_2 (W' = W diag(gamma), s_n, b'_n)
+    if (h->lnfold && layer >= 0) {
+        const bool qkv = name.find("attn.in_proj_weight") != std::string::npos;
+        const bool fc = name.find("mlp.c_fc.weight") != std::string::npos;
+        if (qkv || fc) {
+            LayerW& ly = h->layers[layer];
+            const float* g = qkv ? ly.ln1g : ly.ln2g;
+            const float* be = qkv ? ly.ln1b : ly.ln2b;
+            const float* b = qkv ? ly.bqkv : ly.bfc;
+            launch_lnfold_prep(s, h->dt, w, g, be, b, h->scratch2, qkv ? ly.s_qkv : ly.s_fc,
+                               qkv ? ly.bf_qkv : ly.bf_fc, N, K);
+            launch_pack_weight(s, h->dt, h->scratch2, dst, N, K, Kp);
+            return 0;
+        }
+    }
     launch_pack_weight(s, h->dt, w, dst, N, K, Kp);
     return 0;
 }
@@ -706,6 +837,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->resid16 = !h->mx8 && h->dt == CLIPVIT_F16;
     if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
+    h->lnfold = h->resid16;
+    if (const char* v = getenv("CLIPVIT_LNFOLD")) h->lnfold = h->resid16 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {
@@ -824,7 +957,14 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
         ly.ln2g = h->master[L(i, "ln_2.weight")];
         ly.ln2b = h->master[L(i, "ln_2.bias")];
         maxw = std::max(maxw, 4 * D * D);
+        if (h->lnfold) {
+            if (!ly.s_qkv) HIPCHK(hipMalloc((void**)&ly.s_qkv, 3 * D * sizeof(float)));
+            if (!ly.bf_qkv) HIPCHK(hipMalloc((void**)&ly.bf_qkv, 3 * D * sizeof(float)));
+            if (!ly.s_fc) HIPCHK(hipMalloc((void**)&ly.s_fc, 4 * D * sizeof(float)));
+            if (!ly.bf_fc) HIPCHK(hipMalloc((void**)&ly.bf_fc, 4 * D * sizeof(float)));
+        }
     }
+    if (h->lnfold && !h->scratch2) HIPCHK(hipMalloc((void**)&h->scratch2, 4 * D * D * sizeof(float)));
     if (h->scratch_elems < maxw) {
         if (h->scratch) hipFree(h->scratch);
         HIPCHK(hipMalloc(&h->scratch, maxw * sizeof(float)));
@@ -1047,6 +1187,13 @@ int clipvit_destroy(clipvit_handle* h) {
         hipFree(ly.wproj);
     }
     hipFree(h->scratch);
+    hipFree(h->scratch2);
+    for (auto& ly : h->layers) {
+        hipFree(ly.s_qkv);
+        hipFree(ly.bf_qkv);
+        hipFree(ly.s_fc);
+        hipFree(ly.bf_fc);
+    }
     hipFree(h->Tt);
     hipFree(h->seg_dev);
     for (auto* w : h->pool) free_ws(w);

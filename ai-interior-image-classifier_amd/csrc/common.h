@@ -99,6 +99,14 @@ enum Epi {
     EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
     EPI_GELU_Q8 = 7, // C (MX-fp8) = quickgelu(acc + bias), block scales to sC  (MX-fp8 GEMM)
     EPI_Q8 = 8,      // C (MX-fp8) = acc + bias, block scales to sC             (tests)
+    // LayerNorm folded into the consumer GEMM: A = fp16(x) (the residual
+    // stream, NOT normalised), W' = W diag(gamma); per row mu / rstd from the producer's
+    // 128-column partial statistics st_in; bias = b' = b + W beta, lnf_s = s_n = sum_k W'_nk:
+    EPI_LNF = 9,       // C (T) = rstd (acc - mu s_n) + b'_n                  = LN(x) W^T + b
+    EPI_LNF_GELU = 10, // C (T) = quickgelu(rstd (acc - mu s_n) + b'_n)
+    // residual producer: x (C, f32) += acc + bias; C2 (T) = x; st_out = per-row (mean, M2) of
+    // x over every 128-column group (the consumer's LayerNorm statistics)
+    EPI_RES_STATS = 11,
 };
 
 struct GemmArgs {
@@ -114,7 +122,27 @@ struct GemmArgs {
     const unsigned char* sA;
     const unsigned char* sW;
     unsigned char* sC;
+    // LayerNorm fold (EPI_LNF*, EPI_RES_STATS): np = 128-column groups per row (D / 128)
+    const float* lnf_s;
+    const float2* st_in;
+    float2* st_out;
+    void* C2;
+    int np;
 };
+
+// mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
+// fixed order); eps 1e-5 as CLIP's LayerNorm
+__device__ __forceinline__ void ln_fold_stats(const float2* __restrict__ st, int np, float& mu, float& rstd) {
+    float s = 0.f;
+    for (int p = 0; p < np; ++p) s += st[p].x;
+    mu = s / (float)np;
+    float m2 = 0.f;
+    for (int p = 0; p < np; ++p) {
+        const float d = st[p].x - mu;
+        m2 += st[p].y + 128.f * d * d;
+    }
+    rstd = rsqrtf(m2 / (128.f * (float)np) + 1e-5f);
+}
 
 // Map a launch-order block id to its (m-tile, n-tile). Blocks b, b+8, ... are observed to
 // share an XCD (speed only, never correctness). A 2-D partition gives every XCD group one cell
@@ -233,6 +261,15 @@ void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char
                         const float* b_pre, const float* g1, const float* b1, int B, int N, int D);
 
 void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n);
+// LayerNorm fold of a Linear (W [N, K] fp32, possibly LoRA-merged): Wg = W diag(gamma) (fp32,
+// packed afterwards), s_n = sum_k fp16-or-bf16(Wg_nk), bo_n = b_n + sum_k W_nk beta_k
+void launch_lnfold_prep(hipStream_t s, int dtype, const float* W, const float* gamma, const float* beta,
+                        const float* b, float* Wg, float* s_out, float* b_out, int N, int K);
+// embedding for the folded path: x = ln_pre(cls / patch + pos); x16 = x (16-bit); st = 128-col
+// partial (mean, M2) of x
+void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* st, const float* cls,
+                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D);
+
 
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal = false);

@@ -205,6 +205,101 @@ __device__ __forceinline__ int patch_koff(int kq, int R, int Rw) {
     return (c * R + r) * Rw + j0;
 }
 
+// v[i] = rstd (v[i] - mu s[i]) + b'[i] for the lane's 16 contiguous features (EPI_LNF*)
+__device__ __forceinline__ void lnf_apply(float (&v)[16], const float* __restrict__ s, const float* __restrict__ bp,
+                                          float mu, float rstd) {
+    const float4* s4 = (const float4*)s;
+    const float4* b4 = (const float4*)bp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 ss = s4[i], bb = b4[i];
+        v[4 * i] = rstd * (v[4 * i] - mu * ss.x) + bb.x;
+        v[4 * i + 1] = rstd * (v[4 * i + 1] - mu * ss.y) + bb.y;
+        v[4 * i + 2] = rstd * (v[4 * i + 2] - mu * ss.z) + bb.z;
+        v[4 * i + 3] = rstd * (v[4 * i + 3] - mu * ss.w) + bb.w;
+    }
+}
+
+// EPI_RES_STATS (residual producers out_proj / c_proj): x += acc + bias (fp32, the same additions
+// as EPI_RESID), x16 = x, and per row the (mean, M2) of x over each 128-column group = two
+// adjacent 64-column waves (TN == 64): the 64-column sums are shuffle-reduced over the 4 lanes of
+// a row, exchanged with the partner wave through LDS, then the squared deviations from the
+// group mean the same way (two-pass, no cancellation).
+template <typename T, int FM, int FN, int TM, int TN, int WN>
+__device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&acc)[FN][FM], unsigned char* smem,
+                                                   int m0, int n0, int wm, int wn, int lane) {
+    static_assert(TN == 64 && FN == 4 && WN % 2 == 0, "statistics groups = two 64-wide waves");
+    const int lrow = lane & 15, g = lane >> 4;
+    float* red = (float*)smem;  // [waves][FM][16] partial sums, then the same for M2
+    const int wave = wm * WN + wn, partner = wm * WN + (wn ^ 1);
+    constexpr int NW = 64 * FM * 16;  // floats per exchange region (64 waves max)
+    __builtin_amdgcn_s_barrier();      // every wave is done reading the LDS ring
+    float sum[FM];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const int m = m0 + wm * TM + fm * 16 + lrow;
+        const int n = n0 + wn * TN + 16 * g;
+        float* xr = (float*)a.C + (size_t)min(m, a.M - 1) * a.ldc + n;
+        const float4* b4 = (const float4*)(a.bias + n);
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 bb = b4[i], xo = ((const float4*)xr)[i];
+            f32x4& c = acc[i][fm];
+            c[0] = xo.x + (c[0] + bb.x);
+            c[1] = xo.y + (c[1] + bb.y);
+            c[2] = xo.z + (c[2] + bb.z);
+            c[3] = xo.w + (c[3] + bb.w);
+            s += (c[0] + c[1]) + (c[2] + c[3]);
+        }
+        if (m < a.M) {
+            unsigned char* hr = (unsigned char*)a.C2 + ((size_t)m * a.ldc + n) * 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ((float4*)xr)[i] = make_float4(acc[i][fm][0], acc[i][fm][1], acc[i][fm][2], acc[i][fm][3]);
+            *(uint4*)hr = make_uint4(pack2<T>(acc[0][fm][0], acc[0][fm][1]), pack2<T>(acc[0][fm][2], acc[0][fm][3]),
+                                     pack2<T>(acc[1][fm][0], acc[1][fm][1]), pack2<T>(acc[1][fm][2], acc[1][fm][3]));
+            *(uint4*)(hr + 16) = make_uint4(pack2<T>(acc[2][fm][0], acc[2][fm][1]), pack2<T>(acc[2][fm][2], acc[2][fm][3]),
+                                            pack2<T>(acc[3][fm][0], acc[3][fm][1]), pack2<T>(acc[3][fm][2], acc[3][fm][3]));
+        }
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        sum[fm] = s;
+        if (g == 0) red[(wave * FM + fm) * 16 + lrow] = s;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    float mean[FM];
+#pragma unroll
+    for (int fm = 0; fm < FM; ++fm) {
+        const float ps = red[(partner * FM + fm) * 16 + lrow];
+        mean[fm] = ((wn & 1) ? (ps + sum[fm]) : (sum[fm] + ps)) * (1.0f / 128.f);  // same order in both waves
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = acc[i][fm][r] - mean[fm];
+                q += d * d;
+            }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        sum[fm] = q;
+        if (g == 0) red[NW + (wave * FM + fm) * 16 + lrow] = q;
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if ((wn & 1) == 0 && g == 0) {
+#pragma unroll
+        for (int fm = 0; fm < FM; ++fm) {
+            const int m = m0 + wm * TM + fm * 16 + lrow;
+            if (m < a.M) {
+                const float m2 = sum[fm] + red[NW + (partner * FM + fm) * 16 + lrow];
+                a.st_out[(size_t)m * a.np + (n0 + wn * TN) / 128] = make_float2(mean[fm], m2);
+            }
+        }
+    }
+}
+
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
@@ -354,7 +449,9 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 
     // ---- epilogue (same contract as gemm_nt_kernel) ----
     const int g = lg;
-    if constexpr (SM == 3 && (EPI == EPI_STORE || EPI == EPI_GELU)) {
+    constexpr bool LNF = EPI == EPI_LNF || EPI == EPI_LNF_GELU;
+    constexpr bool GELU = EPI == EPI_GELU || EPI == EPI_F32GELU || EPI == EPI_LNF_GELU;
+    if constexpr (SM == 3 && (EPI == EPI_STORE || EPI == EPI_GELU || LNF)) {
         // Row-contiguous stores staged through LDS: the accumulator layout gives each lane 32 B
         // of one row, so direct stores cover 16 rows x 4 scattered 16-B pieces per
         // wave-instruction; here the tile is first written to LDS (row-major, 16-B chunk
@@ -366,6 +463,8 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) {
             const int r = wm * TM + fm * 16 + lrow;
+            float mu = 0.f, rstd = 1.f;
+            if constexpr (LNF) ln_fold_stats(a.st_in + (size_t)min(m0 + r, mlast) * a.np, a.np, mu, rstd);
 #pragma unroll
             for (int q = 0; q < FN / 4; ++q) {
                 const int nl = wn * TN + q * 64 + 16 * g;
@@ -374,7 +473,8 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                 for (int f = 0; f < 4; ++f)
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[4 * q + f][fm][rr];
-                if (a.bias) {
+                if constexpr (LNF) lnf_apply(v, a.lnf_s + n0 + nl, a.bias + n0 + nl, mu, rstd);
+                else if (a.bias) {
                     const float4* b4 = (const float4*)(a.bias + n0 + nl);
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
@@ -382,7 +482,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                         v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
                     }
                 }
-                if constexpr (EPI == EPI_GELU) {
+                if constexpr (GELU) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
                 }
@@ -407,10 +507,16 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         return;
     }
     unsigned char* const Cb = (unsigned char*)a.C;
+    if constexpr (EPI == EPI_RES_STATS) {
+        res_stats_epilogue<T, FM, FN, TM, TN, WN>(a, acc, smem, m0, n0, wm, wn, lane);
+        return;
+    }
 #pragma unroll
     for (int fm = 0; fm < FM; ++fm) {
         const int m = m0 + wm * TM + fm * 16 + lrow;
         if (m >= a.M) continue;
+        float mu = 0.f, rstd = 1.f;
+        if constexpr (LNF) ln_fold_stats(a.st_in + (size_t)m * a.np, a.np, mu, rstd);
 #pragma unroll
         for (int q = 0; q < FN / 4; ++q) {
             const int n = n0 + wn * TN + q * 64 + 16 * g;
@@ -419,7 +525,9 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
             for (int f = 0; f < 4; ++f)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
-            if constexpr (EPI != EPI_PATCH) {
+            if constexpr (LNF) {
+                lnf_apply(v, a.lnf_s + n, a.bias + n, mu, rstd);
+            } else if constexpr (EPI != EPI_PATCH) {
                 if (a.bias) {
                     const float4* b4 = (const float4*)(a.bias + n);
 #pragma unroll
@@ -429,11 +537,11 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                     }
                 }
             }
-            if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
+            if constexpr (GELU) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
-            if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
+            if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || LNF) {
                 const size_t off = ((size_t)m * a.ldc + n) * 2;
                 *(uint4*)(Cb + off) = (make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
                                        pack2<T>(v[6], v[7])));
@@ -462,26 +570,33 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 }
 
 template <typename T, int BM, int BN, int WM, int WN, int NS, int SM = 0>
-static void launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
+static int launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
     dim3 grid(nwg), block(64 * WM * WN);
-    if constexpr (SM != 0) {  // LDS-staged store builds: production epilogues only
-        switch (epi) {
-            case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE, SM><<<grid, block, 0, s>>>(a); break;
-            case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU, SM><<<grid, block, 0, s>>>(a); break;
-            case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID, SM><<<grid, block, 0, s>>>(a); break;
-            default: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32, SM><<<grid, block, 0, s>>>(a); break;
-        }
-        return;
-    }
+#define PIPE(E) gemm_pipe_kernel<T, BM, BN, WM, WN, NS, E, SM><<<grid, block, 0, s>>>(a)
     switch (epi) {
-        case EPI_STORE: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_STORE><<<grid, block, 0, s>>>(a); break;
-        case EPI_GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_GELU><<<grid, block, 0, s>>>(a); break;
-        case EPI_RESID: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_RESID><<<grid, block, 0, s>>>(a); break;
-        case EPI_PATCH: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32GELU: gemm_pipe_kernel<T, BM, BN, WM, WN, NS, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_STORE: PIPE(EPI_STORE); return 0;
+        case EPI_GELU: PIPE(EPI_GELU); return 0;
+        case EPI_RESID: PIPE(EPI_RESID); return 0;
+        case EPI_LNF: PIPE(EPI_LNF); return 0;
+        case EPI_LNF_GELU: PIPE(EPI_LNF_GELU); return 0;
+        case EPI_RES_STATS:
+            if constexpr (BN / WN == 64 && WN % 2 == 0) {
+                PIPE(EPI_RES_STATS);
+                return 0;
+            }
+            return -1;  // statistics groups need 64-wide waves in pairs
+        case EPI_F32: PIPE(EPI_F32); return 0;
+        case EPI_F32GELU: PIPE(EPI_F32GELU); return 0;
+        case EPI_PATCH:
+            if constexpr (SM == 0) {
+                PIPE(EPI_PATCH);
+                return 0;
+            }
+            return -1;
     }
+#undef PIPE
+    return -1;
 }
 
 // Implicit-GEMM patch embedding on 160x128 tiles (4 waves, two workgroups per CU: the v22 tile
@@ -515,17 +630,18 @@ void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
-static void launch_tile(hipStream_t s, int epi, const GemmArgs& a) {
+static int launch_tile(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
     dim3 grid(nwg), block(64 * WM * WN);
     switch (epi) {
-        case EPI_STORE: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); break;
-        case EPI_GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); break;
-        case EPI_RESID: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
-        case EPI_PATCH: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_PATCH><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
+        case EPI_STORE: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); return 0;
+        case EPI_GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_GELU><<<grid, block, 0, s>>>(a); return 0;
+        case EPI_RESID: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); return 0;
+        case EPI_PATCH: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_PATCH><<<grid, block, 0, s>>>(a); return 0;
+        case EPI_F32: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); return 0;
+        case EPI_F32GELU: gemm_nt_kernel<T, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); return 0;
     }
+    return -1;  // the LayerNorm-fold / statistics epilogues live in the pipelined kernel only
 }
 
 // Auto tile choice: the largest tile whose grid still covers the 256 CUs reasonably.
@@ -544,51 +660,40 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         // ---- single-buffer-per-k-step tiles: shape fallback (pick_variant) ----
         case 1:
             if (a.N % 128) return -1;
-            launch_tile<T, 128, 128, 2, 2>(s, epi, a);
-            return 0;
+            return launch_tile<T, 128, 128, 2, 2>(s, epi, a);
         case 2:
             if (a.N % 128) return -1;
-            launch_tile<T, 256, 128, 4, 2>(s, epi, a);
-            return 0;
+            return launch_tile<T, 256, 128, 4, 2>(s, epi, a);
         case 3:
             if (a.N % 256) return -1;
-            launch_tile<T, 256, 256, 2, 4>(s, epi, a);
-            return 0;
+            return launch_tile<T, 256, 256, 2, 4>(s, epi, a);
         // ---- pipelined ring tiles (the production roles, clipvit.hip gemm()) ----
         case 8:   // 256x256, 8 waves: main launch of the c_fc round split
             if (a.N % 256) return -1;
-            launch_pipe<T, 256, 256, 2, 4, 2>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 256, 256, 2, 4, 2>(s, epi, a);
         case 13:  // 128x128, 8 waves: c_fc (QuickGELU epilogue)
             if (a.N % 128) return -1;
-            launch_pipe<T, 128, 128, 4, 2, 2>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 128, 128, 4, 2, 2>(s, epi, a);
         case 22:  // 160x128, 4 waves, two workgroups per CU: patch embedding
             if (a.N % 128) return -1;
-            launch_pipe<T, 160, 128, 2, 2, 2>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 160, 128, 2, 2, 2>(s, epi, a);
         // ---- LDS-staged row-contiguous 16-bit epilogue (SM = 3) ----
         case 80:  // 256x256: every role of the large-M shapes (B/16, L/14)
             if (a.N % 256) return -1;
-            launch_pipe<T, 256, 256, 2, 4, 2, 3>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 256, 256, 2, 4, 2, 3>(s, epi, a);
         case 81:  // 128x128: tail launch of the c_fc round split
             if (a.N % 128) return -1;
-            launch_pipe<T, 128, 128, 4, 2, 2, 3>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 128, 128, 4, 2, 2, 3>(s, epi, a);
         case 82:  // 160x128, two workgroups per CU: out_proj / c_proj
             if (a.N % 128) return -1;
-            launch_pipe<T, 160, 128, 2, 2, 2, 3>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 160, 128, 2, 2, 2, 3>(s, epi, a);
         case 98:  // 240x256, 12 waves (3 x 4, 80 x 64 per wave): QKV (486 tiles = 1.9 rounds at bs 256)
             if (a.N % 256) return -1;
-            launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);
         // ---- 64x64 tiles, 4-stage ring: the class-token tail's M = B GEMMs ----
         case 90:
             if (a.N % 64) return -1;
-            launch_pipe<T, 64, 64, 2, 1, 4>(s, epi, a);
-            return 0;
+            return launch_pipe<T, 64, 64, 2, 1, 4>(s, epi, a);
     }
     return -1;
 }

@@ -169,6 +169,87 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
     else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
+// ---------------------------------------------------------------------------------------
+// LayerNorm fold. Per row: the (mean, M2) of every 128-column group
+// (lanes 0-31 hold group 2i of the float4 slice i, lanes 32-63 group 2i + 1): sum over the 32
+// lanes, mean, then the squared deviations from it (two-pass), lanes 0 / 32 write.
+template <int V>
+__device__ __forceinline__ void row_stats128(const float4 (&v)[V], float2* __restrict__ st, int lane) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        float s = (v[i].x + v[i].y) + (v[i].z + v[i].w);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o, 64);
+        const float mean = s * (1.0f / 128.f);
+        const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+        float q = (a * a + b * b) + (c * c + d * d);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) q += __shfl_xor(q, o, 64);
+        if ((lane & 31) == 0) st[2 * i + (lane >> 5)] = make_float2(mean, q);
+    }
+}
+
+// x[row] = ln_pre((t == 0 ? class_embedding : patch_row) + pos[t]); x16[row] = x[row] (16-bit);
+// st[row] = its 128-column statistics (block 0's ln_1 is folded into the QKV GEMM)
+template <typename T, int V>
+__global__ __launch_bounds__(256) void embed_stats_kernel(float* __restrict__ x, u16* __restrict__ x16,
+                                                          float2* __restrict__ st, const float* __restrict__ cls,
+                                                          const float* __restrict__ pos, const float* __restrict__ gp,
+                                                          const float* __restrict__ bp, int rows, int N) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const int t = row % N;
+    constexpr int D = 256 * V;
+    float* xr = x + (size_t)row * D;
+    const float* src = t == 0 ? cls : xr;
+    const float* pr = pos + (size_t)t * D;
+    float4 v[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        const float4 a = *(const float4*)(src + c), p = *(const float4*)(pr + c);
+        v[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
+    }
+    ln_row<V>(v, gp, bp, lane, (float)D);
+#pragma unroll
+    for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    store_row16<T, V>(x16 + (size_t)row * D, v, lane);
+    row_stats128<V>(v, st + (size_t)row * (D / 128), lane);
+}
+
+// W' = W diag(gamma) (fp32), s_n = sum_k T(W'_nk) (the values the packed 16-bit operand holds),
+// b'_n = b_n + sum_k W_nk beta_k. One workgroup per row, fixed-order reductions.
+template <typename T>
+__global__ __launch_bounds__(256) void lnfold_prep_kernel(const float* __restrict__ W, const float* __restrict__ gm,
+                                                          const float* __restrict__ be, const float* __restrict__ b,
+                                                          float* __restrict__ Wg, float* __restrict__ so,
+                                                          float* __restrict__ bo, int K) {
+    __shared__ float red[2][256];
+    const int n = blockIdx.x, tid = threadIdx.x;
+    float s = 0.f, bb = 0.f;
+    for (int k = tid; k < K; k += 256) {
+        const float w = W[(size_t)n * K + k], wg = w * gm[k];
+        Wg[(size_t)n * K + k] = wg;
+        s += T::to_f32(T::from_f32(wg));
+        bb += w * be[k];
+    }
+    red[0][tid] = s;
+    red[1][tid] = bb;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) {
+            red[0][tid] += red[0][tid + o];
+            red[1][tid] += red[1][tid + o];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        so[n] = red[0][0];
+        bo[n] = b[n] + red[1][0];
+    }
+}
+
 template <typename T, int V, bool Q8 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x,
                                                         void* __restrict__ h,
@@ -272,6 +353,23 @@ void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
     DISPATCH_V(D, embed_ln_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+}
+
+void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* st, const float* cls,
+                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D) {
+    const int rows = B * N;
+    dim3 grid((rows + 3) / 4), block(256);
+    if (dtype == 2) {
+        DISPATCH_V(D, embed_stats_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N));
+    } else {
+        DISPATCH_V(D, embed_stats_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N));
+    }
+}
+
+void launch_lnfold_prep(hipStream_t s, int dtype, const float* W, const float* gamma, const float* beta,
+                        const float* b, float* Wg, float* s_out, float* b_out, int N, int K) {
+    if (dtype == 2) lnfold_prep_kernel<F16><<<N, 256, 0, s>>>(W, gamma, beta, b, Wg, s_out, b_out, K);
+    else lnfold_prep_kernel<BF16><<<N, 256, 0, s>>>(W, gamma, beta, b, Wg, s_out, b_out, K);
 }
 
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,

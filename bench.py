@@ -56,6 +56,10 @@ def parse():
                    help="MFMA operand type; fp16 meets the 1e-3 logit bar, bf16 does not (DESIGN.md); "
                         "mxfp8 = BASELINE config 5 (MX-fp8 Linears, bf16 attention; bar 2e-2 vs bf16)")
     p.add_argument("--lora-rank", type=int, default=8)
+    p.add_argument("--pixel-dtype", default="model", choices=["model", "fp32"],
+                   help="dtype of the resident input pixels: 'model' = the MFMA operand type, as "
+                        "CLIP's encode_image casts its input (image.type(self.dtype) [3p]); fp32 adds "
+                        "one cast kernel per batch")
     p.add_argument("--inflight", type=int, default=1, help="batches in flight on separate HIP streams")
     p.add_argument("--cpu-seconds", type=float, default=16.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -179,6 +183,8 @@ def main():
     eng.set_text_features(T.numpy(), SEGMENTS)
     gpx = torch.Generator(device=dev).manual_seed(100 + rank)
     px = torch.randn(a.batch, 3, cfg.image_size, cfg.image_size, device=dev, generator=gpx).clamp_(-1.8, 2.2)
+    if a.pixel_dtype == "model":
+        px = px.to(torch.float16 if a.dtype == "fp16" else torch.bfloat16)
     # --inflight batches in flight: step i runs on stream i % n with its own output buffers (the
     # handle hands each in-flight call its own workspace), so one batch's latency-bound tail
     # (class-token block, head) overlaps the next batch's GEMMs. Every step is still one whole
@@ -252,6 +258,7 @@ def main():
         "data": "synthetic (seeded N(0,1) pixels clamped to CLIP-normalised range, seeded CLIP-style weights, synthetic unit text features)",
         "config": {"workload": f"{cfg.name} + merged LoRA r={a.lora_rank} classify (encode_image + cosine head over {N_CLASSES} labels, 6 segments)",
                    "image_size": cfg.image_size, "per_gpu_batch": a.batch, "global_batch": a.batch * world,
+                   "pixel_dtype": str(px.dtype).replace("torch.", ""),
                    "parallelism": (f"dp{world} rehearsal on one GPU, gloo all-gather (not a scaling point)"
                                    if a.share_gpu else f"dp{world}" + (" + RCCL all-gather of logits" if world > 1 else "")),
                    "batches_in_flight": a.inflight},
