@@ -837,8 +837,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->resid16 = !h->mx8 && h->dt == CLIPVIT_F16;
     if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
-    h->lnfold = h->resid16;
-    if (const char* v = getenv("CLIPVIT_LNFOLD")) h->lnfold = h->resid16 && atoi(v) != 0;
+    h->lnfold = h->resid16 && h->D <= 1024;  // <= 8 statistics groups per row (gemm.hip)
+    if (const char* v = getenv("CLIPVIT_LNFOLD")) h->lnfold = h->resid16 && h->D <= 1024 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {

@@ -205,6 +205,16 @@ __device__ __forceinline__ int patch_koff(int kq, int R, int Rw) {
     return (c * R + r) * Rw + j0;
 }
 
+// v[i] += bias[i] for the lane's 16 contiguous features (bias staged in LDS; zero when absent)
+__device__ __forceinline__ void colv_add(float (&v)[16], const float* bias) {
+    const float4* b4 = (const float4*)bias;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 bb = b4[i];
+        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+    }
+}
+
 // v[i] = rstd (v[i] - mu s[i]) + b'[i] for the lane's 16 contiguous features (EPI_LNF*)
 __device__ __forceinline__ void lnf_apply(float (&v)[16], const float* __restrict__ s, const float* __restrict__ bp,
                                           float mu, float rstd) {
@@ -225,8 +235,10 @@ __device__ __forceinline__ void lnf_apply(float (&v)[16], const float* __restric
 // adjacent 64-column waves (TN == 64): the 64-column sums are shuffle-reduced over the 4 lanes of
 // a row, exchanged with the partner wave through LDS, then the squared deviations from the
 // group mean the same way (two-pass, no cancellation).
-template <typename T, int FM, int FN, int TM, int TN, int WN>
-__device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&acc)[FN][FM], unsigned char* smem,
+template <typename T, int FM, int FN, int TM, int TN, int WN, bool PREX>
+__device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&acc)[FN][FM],
+                                                   const float4 (&xpre)[PREX ? FM : 1][4],
+                                                   const float* bias, unsigned char* smem,
                                                    int m0, int n0, int wm, int wn, int lane) {
     static_assert(TN == 64 && FN == 4 && WN % 2 == 0, "statistics groups = two 64-wide waves");
     const int lrow = lane & 15, g = lane >> 4;
@@ -240,11 +252,11 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
         const int m = m0 + wm * TM + fm * 16 + lrow;
         const int n = n0 + wn * TN + 16 * g;
         float* xr = (float*)a.C + (size_t)min(m, a.M - 1) * a.ldc + n;
-        const float4* b4 = (const float4*)(a.bias + n);
+        const float4* b4 = (const float4*)bias;
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float4 bb = b4[i], xo = ((const float4*)xr)[i];
+            const float4 bb = b4[i], xo = PREX ? xpre[PREX ? fm : 0][i] : ((const float4*)xr)[i];
             f32x4& c = acc[i][fm];
             c[0] = xo.x + (c[0] + bb.x);
             c[1] = xo.y + (c[1] + bb.y);
@@ -317,7 +329,16 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     static_assert(A_BYTES % 1024 == 0 && W_BYTES % 1024 == 0, "whole-wave staging pieces");
     constexpr int LPT = LA + LW;  // glds per thread per tile (upper bound when PARTIAL)
     constexpr int STAGE = A_BYTES + W_BYTES;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE];
+    // epilogue operands staged in LDS at kernel start (their global loads overlap the prologue):
+    // per-column bias / b' and s (LNF), per-row mu / rstd (LNF) — the epilogue then issues no
+    // dependent global loads
+    constexpr bool LNF = EPI == EPI_LNF || EPI == EPI_LNF_GELU;
+    constexpr bool COLV = EPI == EPI_STORE || EPI == EPI_GELU || LNF || EPI == EPI_RES_STATS;
+    constexpr int EXTRA = COLV ? 2 * BN * 4 + (LNF ? BM * 8 : 0) : 0;
+    static_assert(BN <= NT && BM <= NT, "one column / row of epilogue operands per thread");
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE + EXTRA];
+    float* const colv = (float*)(smem + NS * STAGE);  // [BN] bias or b', [BN] s
+    float* const rowv = colv + 2 * BN;                // [BM] (mu, rstd)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -398,7 +419,45 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) stage(s, s);
+    // epilogue operands: issued behind the prologue's loads (their first use waits for vmcnt(0),
+    // which with NS = 2 is the prologue's own wait)
+    float cb = 0.f, cs = 0.f;
+    float2 stv[LNF ? 8 : 1];  // np <= 8: width <= 1024 (clipvit_create)
+    if constexpr (COLV) {
+        if (tid < BN) {
+            if (a.bias) cb = a.bias[n0 + tid];
+            if constexpr (LNF) cs = a.lnf_s[n0 + tid];
+        }
+    }
+    if constexpr (LNF) {
+        const float2* st = a.st_in + (size_t)min(m0 + tid, mlast) * a.np;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) stv[p] = st[min(p, a.np - 1)];  // unconditional loads (no per-load branch)
+    }
     wait_tile<LPT, NS>(min(NS - 2, nk - 1));
+    if constexpr (COLV) {
+        if (tid < BN) {
+            colv[tid] = cb;
+            colv[BN + tid] = cs;
+        }
+    }
+    if constexpr (LNF) {
+        if (tid < BM) {
+            float s = 0.f;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) s += p < a.np ? stv[p].x : 0.f;
+            const float mu = s / (float)a.np;
+            float m2 = 0.f;
+#pragma unroll
+            for (int p = 0; p < 8; ++p)
+                if (p < a.np) {
+                    const float d = stv[p].x - mu;
+                    m2 += stv[p].y + 128.f * d * d;
+                }
+            rowv[2 * tid] = mu;
+            rowv[2 * tid + 1] = rsqrtf(m2 / (128.f * (float)a.np) + 1e-5f);
+        }
+    }
     __builtin_amdgcn_s_barrier();
     if (NS - 1 < nk) stage(NS - 1, NS - 1);
 
@@ -438,9 +497,22 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         mfmas(a1, w1);
         interleave();
     }
+    // EPI_RES_STATS: the residual rows this lane updates are loaded during the last tile's MFMAs
+    // (prefetched where the registers allow: FM <= 5, i.e. the 160-row tiles of the N = 768 roles)
+    constexpr bool PREX = EPI == EPI_RES_STATS && FM <= 5;
+    float4 xpre[PREX ? FM : 1][4];
     {   // last tile
         __builtin_amdgcn_s_waitcnt(0xC07F);
         load_frags((nk - 1) % NS, 1, a1, w1);
+        if constexpr (PREX) {
+#pragma unroll
+            for (int fm = 0; fm < FM; ++fm) {
+                const int m = min(m0 + wm * TM + fm * 16 + lrow, mlast);
+                const float4* xr = (const float4*)((const float*)a.C + (size_t)m * a.ldc + n0 + wn * TN + 16 * lg);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) xpre[fm][i] = xr[i];
+            }
+        }
         mfmas(a0, w0);
         interleave();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -449,7 +521,6 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 
     // ---- epilogue (same contract as gemm_nt_kernel) ----
     const int g = lg;
-    constexpr bool LNF = EPI == EPI_LNF || EPI == EPI_LNF_GELU;
     constexpr bool GELU = EPI == EPI_GELU || EPI == EPI_F32GELU || EPI == EPI_LNF_GELU;
     if constexpr (SM == 3 && (EPI == EPI_STORE || EPI == EPI_GELU || LNF)) {
         // Row-contiguous stores staged through LDS: the accumulator layout gives each lane 32 B
@@ -464,7 +535,10 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         for (int fm = 0; fm < FM; ++fm) {
             const int r = wm * TM + fm * 16 + lrow;
             float mu = 0.f, rstd = 1.f;
-            if constexpr (LNF) ln_fold_stats(a.st_in + (size_t)min(m0 + r, mlast) * a.np, a.np, mu, rstd);
+            if constexpr (LNF) {
+                mu = rowv[2 * r];
+                rstd = rowv[2 * r + 1];
+            }
 #pragma unroll
             for (int q = 0; q < FN / 4; ++q) {
                 const int nl = wn * TN + q * 64 + 16 * g;
@@ -473,15 +547,8 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
                 for (int f = 0; f < 4; ++f)
 #pragma unroll
                     for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[4 * q + f][fm][rr];
-                if constexpr (LNF) lnf_apply(v, a.lnf_s + n0 + nl, a.bias + n0 + nl, mu, rstd);
-                else if (a.bias) {
-                    const float4* b4 = (const float4*)(a.bias + n0 + nl);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const float4 bb = b4[i];
-                        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
-                    }
-                }
+                if constexpr (LNF) lnf_apply(v, colv + BN + nl, colv + nl, mu, rstd);
+                else colv_add(v, colv + nl);
                 if constexpr (GELU) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
@@ -508,7 +575,8 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     }
     unsigned char* const Cb = (unsigned char*)a.C;
     if constexpr (EPI == EPI_RES_STATS) {
-        res_stats_epilogue<T, FM, FN, TM, TN, WN>(a, acc, smem, m0, n0, wm, wn, lane);
+        res_stats_epilogue<T, FM, FN, TM, TN, WN, PREX>(a, acc, xpre, colv + wn * TN + 16 * lg, smem, m0, n0, wm, wn,
+                                                        lane);
         return;
     }
 #pragma unroll
@@ -516,7 +584,11 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         const int m = m0 + wm * TM + fm * 16 + lrow;
         if (m >= a.M) continue;
         float mu = 0.f, rstd = 1.f;
-        if constexpr (LNF) ln_fold_stats(a.st_in + (size_t)m * a.np, a.np, mu, rstd);
+        if constexpr (LNF) {
+            const int r = m - m0;
+            mu = rowv[2 * r];
+            rstd = rowv[2 * r + 1];
+        }
 #pragma unroll
         for (int q = 0; q < FN / 4; ++q) {
             const int n = n0 + wn * TN + q * 64 + 16 * g;
@@ -526,7 +598,9 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[4 * f + r] = acc[4 * q + f][fm][r];
             if constexpr (LNF) {
-                lnf_apply(v, a.lnf_s + n, a.bias + n, mu, rstd);
+                lnf_apply(v, colv + BN + (n - n0), colv + (n - n0), mu, rstd);
+            } else if constexpr (COLV) {
+                colv_add(v, colv + (n - n0));
             } else if constexpr (EPI != EPI_PATCH) {
                 if (a.bias) {
                     const float4* b4 = (const float4*)(a.bias + n);
