@@ -24,38 +24,59 @@ def gemm_like(name):
 
 
 def roles_for_trace(rows):
-    """Assign a role to every dispatch of the encoder forward, by order."""
+    """Assign a role to every dispatch of the encoder forward, by order. Between two attention
+    dispatches a block runs out_proj, [ln_2], c_fc (one launch, or main + tail with the
+    whole-round row split), c_proj, [ln_1] (the LayerNorm passes exist only on the unfolded
+    path) and the next block's QKV."""
     out = []
-    layer_seq = ["qkv", "attention", "out", "ln2", "fc", "proj", "ln1"]
-    # c_fc runs as two launches (whole-round row split, DESIGN.md §11) when the dispatch count
-    # between two attention kernels is 8: main rows then tail rows
-    att = [i for i, r in enumerate(rows) if "attention" in r["Kernel_Name"]][:2]
-    if len(att) == 2 and att[1] - att[0] == 8:
-        layer_seq = ["qkv", "attention", "out", "ln2", "fc", "fc_tail", "proj", "ln1"]
-    L = len(layer_seq)
-    pos = None
+    seg = None  # GEMMs seen since the last attention
     for r in rows:
         n = r["Kernel_Name"]
+        if "cast_pixels" in n:
+            out.append("pixel_cast"); continue
+        if gemm_like(n) and "EPI_PATCH" not in n and n.rstrip(")").split(">")[0].split(",")[-1].strip() in ("14", "16", "32"):
+            out.append("patch_gemm"); seg = None; continue
         if "im2col" in n:
-            out.append("im2col"); pos = "patch"; continue
-        if pos == "patch" and gemm_like(n):
-            out.append("patch_gemm"); pos = 0; continue
-        if "embed_ln" in n:
-            out.append("embed_ln"); pos = 0; continue
+            out.append("im2col"); continue
+        if "embed_ln" in n or "embed_stats" in n:
+            out.append("embed"); seg = [] ; continue
         if "gather_cls" in n:  # last block on class-token rows (cls_tail)
-            out.append("cls_tail"); pos = "tail"; continue
-        if pos == "tail" and (gemm_like(n) or "layernorm" in n):
+            out.append("cls_tail"); seg = "tail"; continue
+        if seg == "tail" and (gemm_like(n) or "layernorm" in n):
             out.append("cls_tail"); continue
         if "cls_ln_proj" in n:
-            out.append("head_proj"); pos = None; continue
+            out.append("head_proj"); seg = None; continue
         if "logits_kernel" in n:
             out.append("head_logits"); continue
         if "seg_softmax" in n:
             out.append("head_softmax"); continue
-        if isinstance(pos, int) and (gemm_like(n) or "attention" in n or "layernorm" in n):
-            out.append(layer_seq[pos % L]); pos += 1; continue
+        if "attention" in n:
+            out.append("attention"); seg = []; continue
+        if isinstance(seg, list) and "layernorm" in n:
+            out.append("ln2" if len(seg) == 1 else "ln1"); continue
+        if isinstance(seg, list) and gemm_like(n):
+            seg.append(n)
+            out.append(None)  # resolved below
+            continue
         out.append("other")
-    return out
+    # resolve the GEMMs of each segment: [qkv] after embed; out, fc, [fc_tail], proj, qkv after attention
+    res, i = list(out), 0
+    cur = []
+    def flush(idx_list, after_attention):
+        names = (["out", "fc", "proj", "qkv"] if len(idx_list) == 4 else ["out", "fc", "fc_tail", "proj", "qkv"]) \
+            if after_attention else ["qkv"]
+        for k, ix in enumerate(idx_list):
+            res[ix] = names[k] if k < len(names) else "other"
+    after_att = False
+    for ix, (r, role) in enumerate(zip(rows, out)):
+        if role == "attention" or role == "cls_tail" or role == "head_proj":
+            flush(cur, after_att); cur = []; after_att = role == "attention"
+        elif role == "embed":
+            flush(cur, after_att); cur = []; after_att = False
+        elif role is None:
+            cur.append(ix)
+    flush(cur, after_att)
+    return [x if x is not None else "other" for x in res]
 
 
 def load_rows(path):
@@ -87,9 +108,13 @@ def main():
         return acc
 
     fetch, write = pmc("fetch"), pmc("write")
+    ln_lines = sum(sum(dur[k]) for k in ("ln1", "ln2") if k in dur) / max(1, len(dur.get("qkv", [])) // 12 or 1)
     M, D = 256 * 50, 768
     flops = {"qkv": 2 * M * D * 3 * D, "out": 2 * M * D * D, "fc": 2 * M * D * 4 * D,
              "proj": 2 * M * D * 4 * D, "patch_gemm": 2 * 256 * 49 * 3072 * D}
+    # c_fc with the whole-round row split: the main launch covers 10,752 of the 12,800 rows
+    if "fc_tail" in dur:
+        flops["fc_main"] = flops["fc"] * 10752 / M
     lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16)", "",
              "| role | dispatches | avg us | TFLOP/s | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) |",
              "|---|---|---|---|---|---|"]
