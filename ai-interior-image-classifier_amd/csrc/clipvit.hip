@@ -170,8 +170,6 @@ struct clipvit_handle {
     // become per-row statistics written by the residual producers' epilogues (out_proj, c_proj,
     // embedding) and an affine correction in the QKV / c_fc epilogues; no LayerNorm pass
     bool lnfold = false;
-    // staging loads interleaved among the MFMAs (gemm.hip ILV, variants + 100); CLIPVIT_GEMM_ILV
-    bool ilv = false;
     float* scratch2 = nullptr;  // W diag(gamma) staging for the folded Linears
     // last block on class-token rows only (see cls_tail); CLIPVIT_CLS_PRUNE=0 disables
     bool cls_prune = true;
@@ -374,9 +372,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             if (c.st_in) c.st_in += (size_t)m1 * c.np;
             c.M = M - (int)m1;
             c.xcd_n = 0;
-            const int vm = h->ilv ? 100 + h->split_main : h->split_main;
-            const int vt = h->split_tail ? (h->ilv ? 100 + h->split_tail : h->split_tail) : variant;
-            if (launch_gemm(s, h->dt, epi, b, vm) == 0 && launch_gemm(s, h->dt, epi, c, vt) == 0)
+            if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 &&
+                launch_gemm(s, h->dt, epi, c, h->split_tail ? h->split_tail : variant) == 0)
                 return 0;
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
@@ -385,8 +382,6 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     if (!h->var_forced && role != R_PATCH &&
         (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu)))
         variant = 80;
-    if (h->ilv && (variant == 8 || variant == 13 || (variant >= 80 && variant <= 82) || variant == 98))
-        variant += 100;
     // a tuned variant that does not tile this shape falls back to the shape-based choice
     if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -842,7 +837,6 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->resid16 = !h->mx8 && h->dt == CLIPVIT_F16;
     if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_GEMM_ILV")) h->ilv = atoi(v) != 0;
     // off by default: measured slower (the residual epilogues run in lockstep
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
     h->lnfold = false;  // <= 8 statistics groups per row (gemm.hip) when enabled

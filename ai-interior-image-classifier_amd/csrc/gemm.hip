@@ -313,10 +313,7 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
 }
 
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
-// ILV = 1: the next tile's global->LDS loads are issued among the second substep's MFMAs
-// (after its fragment reads) instead of as one burst right after the barrier, so a wave's
-// LDS-DMA issue slots overlap the partner wave's matrix work.
-template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0, int ILV = 0>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0>
 __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
@@ -476,23 +473,6 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         __builtin_amdgcn_sched_group_barrier(0x008, NMF - NFR, 0);
     };
     static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
-    // ILV: fragment reads one per MFMA, then the staging loads one per MFMA, then the rest
-    auto interleave_ld = [&]() {
-        constexpr int NV = (NMF - NFR) < LPT ? (NMF - NFR) : LPT;
-#pragma unroll
-        for (int i = 0; i < NFR; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
-        }
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM (global_load_lds)
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, NMF - NFR - NV, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, LPT - NV, 0);
-    };
-
     auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
@@ -509,21 +489,12 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         mfmas(a0, w0);
         interleave();
         __builtin_amdgcn_s_waitcnt(0xC07F);                  // a1/w1 landed: stage kt fully read
-        wait_tile<LPT, NS>(ILV ? NS - 2 : min(NS - 2, nk - 2 - kt));  // tile kt+1 landed (own loads)
+        wait_tile<LPT, NS>(min(NS - 2, nk - 2 - kt));       // tile kt+1 landed (own loads)
         __builtin_amdgcn_s_barrier();                        // ... and everyone else's
-        if constexpr (ILV) {
-            load_frags((kt + 1) % NS, 0, a0, w0);
-            // the stage just freed is refilled with tile kt + NS (clamped: a tile past the end
-            // reloads the last one into a stage nobody reads again), interleaved with the MFMAs
-            stage(cur, min(kt + NS, nk - 1));
-            mfmas(a1, w1);
-            interleave_ld();
-        } else {
-            if (kt + NS < nk) stage(cur, kt + NS);           // refill the stage just freed
-            load_frags((kt + 1) % NS, 0, a0, w0);
-            mfmas(a1, w1);
-            interleave();
-        }
+        if (kt + NS < nk) stage(cur, kt + NS);               // refill the stage just freed
+        load_frags((kt + 1) % NS, 0, a0, w0);
+        mfmas(a1, w1);
+        interleave();
     }
     // EPI_RES_STATS: the residual rows this lane updates are loaded during the last tile's MFMAs
     // (prefetched where the registers allow: FM <= 5, i.e. the 160-row tiles of the N = 768 roles)
@@ -671,11 +642,11 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     }
 }
 
-template <typename T, int BM, int BN, int WM, int WN, int NS, int SM = 0, int ILV = 0>
+template <typename T, int BM, int BN, int WM, int WN, int NS, int SM = 0>
 static int launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
     dim3 grid(nwg), block(64 * WM * WN);
-#define PIPE(E) gemm_pipe_kernel<T, BM, BN, WM, WN, NS, E, SM, 0, ILV><<<grid, block, 0, s>>>(a)
+#define PIPE(E) gemm_pipe_kernel<T, BM, BN, WM, WN, NS, E, SM><<<grid, block, 0, s>>>(a)
     switch (epi) {
         case EPI_STORE: PIPE(EPI_STORE); return 0;
         case EPI_GELU: PIPE(EPI_GELU); return 0;
@@ -792,25 +763,6 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         case 98:  // 240x256, 12 waves (3 x 4, 80 x 64 per wave): QKV (486 tiles = 1.9 rounds at bs 256)
             if (a.N % 256) return -1;
             return launch_pipe<T, 240, 256, 3, 4, 2, 3>(s, epi, a);
-        // ---- the same tiles with the staging loads interleaved among the MFMAs (ILV) ----
-        case 108:
-            if (a.N % 256) return -1;
-            return launch_pipe<T, 256, 256, 2, 4, 2, 0, 1>(s, epi, a);
-        case 113:
-            if (a.N % 128) return -1;
-            return launch_pipe<T, 128, 128, 4, 2, 2, 0, 1>(s, epi, a);
-        case 180:
-            if (a.N % 256) return -1;
-            return launch_pipe<T, 256, 256, 2, 4, 2, 3, 1>(s, epi, a);
-        case 181:
-            if (a.N % 128) return -1;
-            return launch_pipe<T, 128, 128, 4, 2, 2, 3, 1>(s, epi, a);
-        case 182:
-            if (a.N % 128) return -1;
-            return launch_pipe<T, 160, 128, 2, 2, 2, 3, 1>(s, epi, a);
-        case 198:
-            if (a.N % 256) return -1;
-            return launch_pipe<T, 240, 256, 3, 4, 2, 3, 1>(s, epi, a);
         // ---- 64x64 tiles, 4-stage ring: the class-token tail's M = B GEMMs ----
         case 90:
             if (a.N % 64) return -1;
