@@ -108,16 +108,22 @@ def main():
         return acc
 
     fetch, write = pmc("fetch"), pmc("write")
-    ln_lines = sum(sum(dur[k]) for k in ("ln1", "ln2") if k in dur) / max(1, len(dur.get("qkv", [])) // 12 or 1)
     M, D = 256 * 50, 768
-    flops = {"qkv": 2 * M * D * 3 * D, "out": 2 * M * D * D, "fc": 2 * M * D * 4 * D,
-             "proj": 2 * M * D * 4 * D, "patch_gemm": 2 * 256 * 49 * 3072 * D}
-    # c_fc with the whole-round row split: the main launch covers 10,752 of the 12,800 rows
+    # (rows, N, K) of each GEMM role at bs 256; c_fc with the whole-round row split: the main
+    # launch covers rows [0, 10752), the tail launch the other 2,048
+    shapes = {"qkv": (M, 3 * D, D), "out": (M, D, D), "proj": (M, D, 4 * D), "patch_gemm": (256 * 49, D, 3072)}
+    shapes["fc"] = (10752, 4 * D, D) if "fc_tail" in dur else (M, 4 * D, D)
     if "fc_tail" in dur:
-        flops["fc_main"] = flops["fc"] * 10752 / M
+        shapes["fc_tail"] = (M - 10752, 4 * D, D)
+    flops = {r: 2 * m * n * k for r, (m, n, k) in shapes.items()}
+    # algorithmic bytes per launch: A once, W once, 16-bit C once
+    algo = {r: 2 * (m * k + n * k + m * n) for r, (m, n, k) in shapes.items()}
     lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16)", "",
-             "| role | dispatches | avg us | TFLOP/s | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) |",
-             "|---|---|---|---|---|---|"]
+             "TFLOP/s = the launch's own FLOPs / rocprof average duration. Algorithmic MB = A + W + C",
+             "(16-bit) once. PMC MB = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction; L2 misses served",
+             "from the Infinity Cache are counted, writes still dirty in L2 at kernel end are not).", "",
+             "| role | dispatches | avg us | TFLOP/s | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic |",
+             "|---|---|---|---|---|---|---|---|"]
     traffic = {}
     for role in sorted(dur, key=lambda k: -sum(dur[k])):
         d = dur[role]
@@ -126,13 +132,17 @@ def main():
         fb = 2 * sum(fetch[role]) / len(fetch[role]) * 1024 / 1e6 if fetch.get(role) else float("nan")
         wb = sum(write[role]) / len(write[role]) * 1024 / 1e6 if write.get(role) else float("nan")
         traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6}
-        lines.append(f"| {role} | {len(d)} | {avg:.1f} | {tf} | {fb:.1f} | {wb:.1f} |")
+        al = f"{algo[role] / 1e6:.1f}" if role in algo else ""
+        ratio = f"{(fb + wb) * 1e6 / algo[role]:.2f}" if role in algo else ""
+        lines.append(f"| {role} | {len(d)} | {avg:.1f} | {tf} | {fb:.1f} | {wb:.1f} | {al} | {ratio} |")
     if "fc_tail" in traffic:  # one c_fc invocation = main + tail launch
         a, b = traffic["fc"], traffic.pop("fc_tail")
         traffic["fc"] = {k: a[k] + b[k] for k in a}
         t = traffic["fc"]
-        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {flops['fc'] / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
-                     f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} |")
+        fl, al = flops["fc"] + flops["fc_tail"], algo["fc"] + algo["fc_tail"]
+        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
+                     f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} | {al / 1e6:.1f} | "
+                     f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     mlp = [traffic[r] for r in ("fc", "proj") if r in traffic]
     entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
