@@ -448,35 +448,38 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     unsigned char* base = (unsigned char*)w->u;
     float* xc = (float*)base;
     u16* hc = (u16*)(base + (size_t)B * D * 4);
-    u16* yc = hc + (size_t)B * D;
-    u16* uc = yc + (size_t)B * D;
-    int rc;
+    u16* uc = hc + (size_t)B * D;
+    // split-K partial products: the full-M qkv buffer is dead once gather_cls has run
+    // (S * B * 4D * 4 bytes <= B * N * 3D * 2 for S <= 8, N >= 50)
+    float* part = (float*)w->qkv;
     launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D);
-    auto g0 = [&](int epi, const void* A, const void* W, const float* bias, void* C, int n, int k) {
+    // M = B rows: 64x64 tiles alone give B/64 x N/64 workgroups whose K-long dependency chains
+    // (48 k-tiles for c_proj) bound the tail, so each GEMM splits K into S slices (fixed per
+    // shape: results do not depend on B) summed in slice order by the following kernel.
+    // Measured tail 0.064 ms with one K chain (c_proj alone 27 us).
+    auto g0 = [&](const void* A, const void* W, int n, int k, int& S) {
+        S = 1;
+        for (int c : {8, 4, 2})
+            if (k % (64 * c) == 0 && k / c >= 192) { S = c; break; }
         GemmArgs a{};
-        a.A = A; a.W = W; a.bias = bias; a.C = C;
-        a.M = B; a.N = n; a.K = k; a.ldc = n;
-        // 64x64 tiles for M = B rows (the most workgroups); the pipelined 4-stage ring (v90)
-        // keeps 3 k-tiles in flight for the cold, long-K c_proj weights: tail 0.080 -> 0.063 ms
-        if (launch_gemm(s, h->dt, epi, a, h->tail_var) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
+        a.A = A; a.W = W; a.bias = nullptr; a.C = part;
+        a.M = B; a.N = n; a.K = k; a.ldc = n; a.ksplit = S;
+        if (launch_gemm(s, h->dt, EPI_F32, a, h->tail_var) != 0) {
             g_err = "cls tail gemm: unsupported shape";
             return CLIPVIT_E_INVALID;
         }
         return 0;
     };
-    if (h->resid16) {
-        if ((rc = g0(EPI_STORE, hc, ly.wout, ly.bout, yc, D, D))) return rc;
-        if (prof) prof->mark(s, F_TAIL);
-        launch_add_layernorm(s, h->dt, xc, yc, hc, ly.ln2g, ly.ln2b, B, D);
-    } else {
-        if ((rc = g0(EPI_RESID, hc, ly.wout, ly.bout, xc, D, D))) return rc;
-        if (prof) prof->mark(s, F_TAIL);
-        launch_layernorm(s, h->dt, xc, hc, ly.ln2g, ly.ln2b, B, D);
-    }
+    int rc, S;
+    if ((rc = g0(hc, ly.wout, D, D, S))) return rc;
     if (prof) prof->mark(s, F_TAIL);
-    if ((rc = g0(EPI_GELU, hc, ly.wfc, ly.bfc, uc, 4 * D, D))) return rc;
+    launch_splitk_resid_ln(s, h->dt, xc, part, S, ly.bout, hc, ly.ln2g, ly.ln2b, B, D);
     if (prof) prof->mark(s, F_TAIL);
-    if ((rc = g0(EPI_RESID, uc, ly.wproj, ly.bproj, xc, D, 4 * D))) return rc;
+    if ((rc = g0(hc, ly.wfc, 4 * D, D, S))) return rc;
+    launch_splitk_gelu(s, h->dt, part, S, ly.bfc, uc, B, 4 * D);
+    if (prof) prof->mark(s, F_TAIL);
+    if ((rc = g0(uc, ly.wproj, D, 4 * D, S))) return rc;
+    launch_splitk_resid_ln(s, h->dt, xc, part, S, ly.bproj, nullptr, nullptr, nullptr, B, D);
     if (prof) prof->mark(s, F_TAIL);
     launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E);
     if (prof) prof->mark(s, F_HEAD);
@@ -1223,7 +1226,11 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // LDS-staged 16-bit-output variants (80-82, 98), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98;
-    if (staged || epi >= 10) {
+    if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
+        a.ksplit = epi - 20;
+        a.bias = nullptr;
+        rc = launch_gemm(s, dtype, EPI_F32, a, variant);
+    } else if (staged || epi >= 10) {
         if (epi >= 10) epi -= 10;
         if (epi == 2) {
             hipFreeAsync(Wp, s);

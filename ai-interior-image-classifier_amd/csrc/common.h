@@ -128,6 +128,9 @@ struct GemmArgs {
     float2* st_out;
     void* C2;
     int np;
+    // split-K (EPI_F32 on the pipelined tiles only): grid.y = ksplit slices of K / ksplit each;
+    // slice z writes its fp32 partial (no bias) to C + z * M * ldc. 0 / 1 = no split
+    int ksplit;
 };
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
@@ -251,6 +254,13 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
                           const float* b, int rows, int D);
 // x' = x + y (+ y2); h = LayerNorm(x'). y2 == nullptr: x' is NOT stored (deferred: the next
 // call adds both branch outputs in the same order); y2 != nullptr: x' is stored.
+// split-K reduction of the class-token tail (cls_tail): t = P[0] + ... + P[S-1] (fixed order),
+// x += t + bias; with h != nullptr also h = LayerNorm(x) (16-bit)
+void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, int S, const float* bias,
+                            void* h, const float* g, const float* b, int rows, int D);
+// u = quickgelu(P[0] + ... + P[S-1] + bias) (16-bit), [rows, n]
+void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const float* bias, void* u, int rows,
+                        int n);
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
                                    void* h, const float* g, const float* b, int rows, int D);
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D);

@@ -376,10 +376,13 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         const int row = p >> 7, c = ((p >> 4) & 7) ^ (row & 7);
         wsrc[r] = (size_t)(n0 + row) * ldb + c * 16;
     }
+    // split-K slice (EPI_F32 only, launch_pipe): k-tiles [kz * nk, kz * nk + nk) of the row
+    const int kz = a.ksplit > 1 ? (int)blockIdx.y : 0;
+    const size_t kbase = a.ksplit > 1 ? (size_t)kz * (a.K / a.ksplit) * 2 : 0;
     auto stage = [&](int buf, int kt) {
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
-        const size_t kofs = (size_t)kt * 128;
+        const size_t kofs = kbase + (size_t)kt * 128;
 #pragma unroll
         for (int r = 0; r < LA; ++r)
             if (r * NT * 16 + wave * 1024 < A_BYTES) {  // wave-uniform
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     // Ring protocol: tile t lives in stage t % NS. Prologue issues tiles 0..NS-2; the stage of
     // tile t-1 is refilled with tile t-1+NS right after the barrier that follows every wave's
     // last ds_read of tile t-1 (lgkmcnt(0) before that barrier).
-    const int nk = a.K >> 6;
+    const int nk = (a.ksplit > 1 ? a.K / a.ksplit : a.K) >> 6;
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) stage(s, s);
@@ -572,7 +575,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
         }
         return;
     }
-    unsigned char* const Cb = (unsigned char*)a.C;
+    unsigned char* const Cb = (unsigned char*)a.C + (EPI == EPI_F32 ? (size_t)kz * a.M * a.ldc * 4 : 0);
     if constexpr (EPI == EPI_RES_STATS) {
         res_stats_epilogue<T, FM, FN, TM, TN, WN, PREX>(a, acc, xpre, colv + wn * TN + 16 * lg, smem, m0, n0, wm, wn,
                                                         lane);
@@ -645,7 +648,8 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
 template <typename T, int BM, int BN, int WM, int WN, int NS, int SM = 0>
 static int launch_pipe(hipStream_t s, int epi, const GemmArgs& a) {
     const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
-    dim3 grid(nwg), block(64 * WM * WN);
+    if (a.ksplit > 1 && (epi != EPI_F32 || a.K % (64 * a.ksplit) != 0)) return -1;
+    dim3 grid(nwg, a.ksplit > 1 ? a.ksplit : 1), block(64 * WM * WN);
 #define PIPE(E) gemm_pipe_kernel<T, BM, BN, WM, WN, NS, E, SM><<<grid, block, 0, s>>>(a)
     switch (epi) {
         case EPI_STORE: PIPE(EPI_STORE); return 0;
@@ -773,6 +777,8 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
+    // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
+    if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);
     return launch_t<BF16>(s, epi, a, variant);
 }

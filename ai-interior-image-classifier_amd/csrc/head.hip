@@ -33,49 +33,57 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
                                            int n, const float* __restrict__ gm,
                                            const float* __restrict__ bt, float* dst,
                                            float* __restrict__ norm_out) {
+    // the wave's HR / 4 rows: every load of every row is issued before the first reduction (one
+    // memory round trip per wave instead of one per row)
+    constexpr int RW = HR / 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nv = n >> 6;
-    for (int i = wave; i < HR; i += 4) {
-        const int b = b0 + i;
+    float v[RW][HMAXD];
+#pragma unroll
+    for (int rr = 0; rr < RW; ++rr) {
+        const int b = min(b0 + wave + 4 * rr, B - 1);  // rows past B: clamped load, zero row below
+        const float* r = src + (size_t)b * stride;
+#pragma unroll
+        for (int j = 0; j < HMAXD; ++j) {  // unconditional loads (clamped address), then select
+            const float t = r[lane + 64 * min(j, nv - 1)];
+            v[rr][j] = j < nv ? t : 0.f;
+        }
+    }
+#pragma unroll
+    for (int rr = 0; rr < RW; ++rr) {
+        const int i = wave + 4 * rr, b = b0 + i;
         float* d = dst + i * (n + 4);  // rows padded by 4 floats: the product's 4 image reads hit distinct banks
         if (b >= B) {
             for (int c = lane; c < n; c += 64) d[c] = 0.f;
             continue;
         }
-        const float* r = src + (size_t)b * stride;
-        float v[HMAXD];
-#pragma unroll
-        for (int j = 0; j < HMAXD; ++j) {  // unconditional loads (clamped address), then select
-            const float t = r[lane + 64 * min(j, nv - 1)];
-            v[j] = j < nv ? t : 0.f;
-        }
         if constexpr (MODE == 0) {
             float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < HMAXD; ++j) s += v[j];
+            for (int j = 0; j < HMAXD; ++j) s += v[rr][j];
             const float mean = wave_sum(s) / n;
             float q = 0.f;
 #pragma unroll
             for (int j = 0; j < HMAXD; ++j)
-                if (j < nv) q += (v[j] - mean) * (v[j] - mean);
+                if (j < nv) q += (v[rr][j] - mean) * (v[rr][j] - mean);
             const float rstd = rsqrtf(wave_sum(q) / n + 1e-5f);
 #pragma unroll
             for (int j = 0; j < HMAXD; ++j)
                 if (j < nv) {
                     const int c = lane + 64 * j;
-                    d[c] = (v[j] - mean) * rstd * gm[c] + bt[c];
+                    d[c] = (v[rr][j] - mean) * rstd * gm[c] + bt[c];
                 }
         } else {
             float q = 0.f;
 #pragma unroll
-            for (int j = 0; j < HMAXD; ++j) q += v[j] * v[j];
+            for (int j = 0; j < HMAXD; ++j) q += v[rr][j] * v[rr][j];
             const float inv = 1.0f / sqrtf(wave_sum(q));
 #pragma unroll
             for (int j = 0; j < HMAXD; ++j)
                 if (j < nv) {
                     const int c = lane + 64 * j;
-                    d[c] = v[j] * inv;
-                    if (norm_out) norm_out[(size_t)b * n + c] = v[j] * inv;
+                    d[c] = v[rr][j] * inv;
+                    if (norm_out) norm_out[(size_t)b * n + c] = v[rr][j] * inv;
                 }
         }
     }

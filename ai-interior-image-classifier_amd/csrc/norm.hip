@@ -322,6 +322,67 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
     }
 }
 
+// Split-K reduction of the class-token tail's GEMMs (clipvit.hip cls_tail): P = S fp32 partial
+// products [S][rows][D] (no bias), summed in slice order; x += (t + bias); optionally
+// h = LayerNorm(x). One wave per row (the tail has B rows: latency, not bandwidth).
+template <typename T, int V, bool LN>
+__global__ __launch_bounds__(256) void splitk_resid_ln_kernel(float* __restrict__ x, const float* __restrict__ P, int S,
+                                                              const float* __restrict__ bias, u16* __restrict__ h,
+                                                              const float* __restrict__ gm,
+                                                              const float* __restrict__ bt, int rows) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    constexpr int D = 256 * V;
+    const size_t ps = (size_t)rows * D;
+    float* xr = x + (size_t)row * D;
+    const float* pr = P + (size_t)row * D;
+    float4 v[V], t[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
+        t[i] = *(const float4*)(pr + (lane + 64 * i) * 4);
+    }
+    for (int z = 1; z < S; ++z) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float4 q = *(const float4*)(pr + z * ps + (lane + 64 * i) * 4);
+            t[i].x += q.x; t[i].y += q.y; t[i].z += q.z; t[i].w += q.w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float4 bb = *(const float4*)(bias + (lane + 64 * i) * 4);
+        v[i].x += t[i].x + bb.x; v[i].y += t[i].y + bb.y; v[i].z += t[i].z + bb.z; v[i].w += t[i].w + bb.w;
+        *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    }
+    if constexpr (LN) {
+        ln_row<V>(v, gm, bt, lane, (float)D);
+        store_row16<T, V>(h + (size_t)row * D, v, lane);
+    }
+}
+
+// u = quickgelu(P[0] + ... + P[S-1] + bias) -> 16-bit, [rows, n]; 4 columns per thread
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restrict__ P, int S,
+                                                          const float* __restrict__ bias, u16* __restrict__ u,
+                                                          int rows, int n) {
+    const size_t i4 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t tot = (size_t)rows * n;
+    if (i4 * 4 >= tot) return;
+    const size_t e = i4 * 4;
+    float4 t = *(const float4*)(P + e);
+    for (int z = 1; z < S; ++z) {
+        const float4 q = *(const float4*)(P + z * tot + e);
+        t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
+    }
+    const float4 bb = *(const float4*)(bias + e % n);
+    float v[4] = {t.x + bb.x, t.y + bb.y, t.z + bb.z, t.w + bb.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[k]));
+    *(uint2*)(u + e) = make_uint2(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]));
+}
+
 // add_layernorm_kernel runs one row per wave (RPW = 1): two rows per wave measured no faster
 // in-model in round 1 (LayerNorm family 0.447 -> 0.453 ms per forward at bs 256); one row per
 // wave already streams at ~5.7 TB/s.
@@ -394,6 +455,28 @@ static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2
     dim3 grid((rows + 3) / 4), block(256);
     if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
     else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
+}
+
+void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, int S, const float* bias,
+                            void* h, const float* g, const float* b, int rows, int D) {
+    dim3 grid((rows + 3) / 4), block(256);
+    if (h) {
+        if (dtype == 2) {
+            DISPATCH_V(D, splitk_resid_ln_kernel<F16, V, true><<<grid, block, 0, s>>>(x, P, S, bias, (u16*)h, g, b, rows));
+        } else {
+            DISPATCH_V(D, splitk_resid_ln_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, P, S, bias, (u16*)h, g, b, rows));
+        }
+    } else {
+        DISPATCH_V(D, splitk_resid_ln_kernel<F16, V, false><<<grid, block, 0, s>>>(x, P, S, bias, nullptr, g, b, rows));
+    }
+}
+
+void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const float* bias, void* u, int rows,
+                        int n) {
+    const size_t n4 = (size_t)rows * n / 4;
+    dim3 grid((unsigned)((n4 + 255) / 256)), block(256);
+    if (dtype == 2) splitk_gelu_kernel<F16><<<grid, block, 0, s>>>(P, S, bias, (u16*)u, rows, n);
+    else splitk_gelu_kernel<BF16><<<grid, block, 0, s>>>(P, S, bias, (u16*)u, rows, n);
 }
 
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,

@@ -212,7 +212,9 @@ int clipvit_resample_plan(int in_size, int out_size, int* ksize, int* bounds, in
 /* C[M,N] = A[M,K] @ W[N,K]^T + bias.  A_dev: 16-bit (`dtype` BF16/F16) row-major;
  * W_dev: fp32 [N,K] natural row order (packed to `dtype` internally, as clipvit_load_weights
  * does); bias fp32 [N] or NULL; C fp32 [M,N]. epi: 0 = store, 1 = QuickGELU then store,
- * 2 = accumulate into C (residual add). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
+ * 2 = accumulate into C (residual add), 10 / 11 = 16-bit store / QuickGELU widened to fp32,
+ * 20 + S = split-K into S slices (pipelined variants >= 8; C holds [S][M][N] fp32 partial
+ * products without bias; K % (64 S) == 0 — the class-token tail's GEMMs). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
  * N % 256 for variant 3). variant % 100 selects the tile kernel (0 auto; the table in
  * csrc/gemm.hip pick/launch_gemm); variant / 100 the block->XCD mapping
  * (0/1 = 1-D bijective remap, 2 = 4x2 (M-band, N-half) partition; pipelined variants only).

@@ -86,6 +86,37 @@ def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     assert err < 2e-3, err
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("variant,M,N,K,S", [(90, 256, 768, 3072, 8), (90, 67, 3072, 768, 4),
+                                             (90, 9, 768, 768, 4), (90, 256, 1024, 1024, 4),
+                                             (8, 300, 512, 1024, 2), (82, 333, 768, 1536, 3)])
+def test_gemm_split_k(gpu, dtype, variant, M, N, K, S):
+    """Split-K (the class-token tail's GEMMs): slice z of grid.y writes the fp32 partial of
+    k in [z K/S, (z + 1) K/S) to C[z]; each partial is checked against its own K slice, so a
+    slice offset error cannot cancel in the sum. Ragged M included."""
+    g = torch.Generator(device=gpu).manual_seed(M + N + K + S)
+    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    C = torch.full((S * M, N), float("nan"), device=gpu)
+    C = E.gemm_test(A, W, None, epi=20 + S, variant=variant, C=C).reshape(S, M, N)
+    ks = K // S
+    for z in range(S):
+        ref = _ref_gemm(A[:, z * ks:(z + 1) * ks], W[:, z * ks:(z + 1) * ks], None, 0)
+        err = (C[z] - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-3, (z, err)
+
+
+def test_gemm_split_k_refuses_bad_slices(gpu):
+    """K not divisible into 64-deep slices, or a non-pipelined tile: the library refuses."""
+    A = torch.zeros(64, 768, device=gpu, dtype=torch.float16)
+    W = torch.zeros(64, 768, device=gpu)
+    C = torch.zeros(8 * 64, 64, device=gpu)
+    with pytest.raises(Exception):
+        E.gemm_test(A, W, None, epi=20 + 8, variant=90, C=C)  # 768 / 8 = 96: not a multiple of 64
+    with pytest.raises(Exception):
+        E.gemm_test(A, W, None, epi=20 + 4, variant=1, C=C)
+
+
 @pytest.mark.parametrize("epi", [0, 1, 2])
 def test_gemm_epilogues(gpu, epi):
     dtype = torch.bfloat16

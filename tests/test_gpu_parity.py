@@ -158,11 +158,13 @@ def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
 def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
-    """The last block on class-token rows only (CLIPVIT_CLS_PRUNE) and, on the unfolded path,
-    the deferred residual store (CLIPVIT_DEFER_X) execute the same per-row fp32 operations in
+    """The deferred residual store (CLIPVIT_DEFER_X) executes the same per-row fp32 operations in
     the same order, so the features equal the full computation's bit for bit (B/32 and the
-    N = 197 B/16 geometry), with the LayerNorm fold (fp16 default, CLIPVIT_LNFOLD) and without.
-    The folded and unfolded paths agree to rounding (different but equivalent arithmetic)."""
+    N = 197 B/16 geometry), with the last block on class-token rows only (CLIPVIT_CLS_PRUNE) and
+    without, with the LayerNorm fold (CLIPVIT_LNFOLD) and without. The unfolded class-token tail
+    splits K of its three GEMMs (fp32 partials summed in slice order, no 16-bit branch output),
+    so pruned and full last blocks agree to rounding; the folded tail stays bit-identical. The
+    folded and unfolded paths agree to rounding (different but equivalent arithmetic)."""
     for cfg, B in ((C.VIT_B32, 67), (C.VIT_B16, 9)):
         sd = synthetic_state_dict(cfg, 0)
         ad = synthetic_adapters(cfg, rank=8)
@@ -176,15 +178,24 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
             eng = VisionEngine(cfg, 0, dtype, max_batch=B)
             eng.load_state_dict(sd)
             eng.load_lora(ad)
-            groups.setdefault(fold, []).append(eng.encode_image(px).clone())
+            # the fold applies to the fp16 path only (bf16 ignores CLIPVIT_LNFOLD)
+            key = "fold" if fold == "1" and dtype == "fp16" else "prune" + prune
+            groups.setdefault(key, []).append(eng.encode_image(px).clone())
             torch.cuda.synchronize()
             eng.close()
-        for fold, outs in groups.items():
+        for key, outs in groups.items():
             for o in outs[1:]:
-                assert torch.equal(outs[0], o), (cfg.name, dtype, fold)
-        f1, f0 = groups["1"][0], groups["0"][0]
-        rel = ((f1 - f0).norm(dim=-1) / f0.norm(dim=-1)).max().item()
-        assert rel < (3e-3 if dtype == "fp16" else 2e-2), (cfg.name, dtype, rel)
+                assert torch.equal(outs[0], o), (cfg.name, dtype, key)
+
+        def rel(a, b):
+            return ((a - b).norm(dim=-1) / b.norm(dim=-1)).max().item()
+
+        split = rel(groups["prune1"][0], groups["prune0"][0])
+        assert split < (5e-4 if dtype == "fp16" else 5e-3), (cfg.name, dtype, split)
+        print(f"[{cfg.name} {dtype}] split-K class-token tail vs full last block: rel {split:.2e}")
+        if "fold" in groups:
+            f1, f0 = groups["fold"][0], groups["prune0"][0]
+            assert rel(f1, f0) < 3e-3, (cfg.name, dtype, rel(f1, f0))
 
 
 @pytest.mark.parametrize("dtype,pdt", [("fp16", torch.float16), ("bf16", torch.bfloat16)])
