@@ -140,6 +140,20 @@ def parity_check(eng, px, T, cfg, n: int = 4):
     return float((np.abs(lg - lr).max(axis=1) / np.abs(lr).max(axis=1)).max())
 
 
+def parity_vs_bf16(eng, px, T, cfg, dev, n: int = 64):
+    """BASELINE config 5's own bar: MX-fp8 logits against the bf16 engine on the same weights
+    (LoRA merged) and the same n images of the benched batch, per image max|dlogit| / max|logit|."""
+    ref = VisionEngine(cfg, dev, "bf16", max_batch=n)
+    ref.load_state_dict(synthetic_state_dict(cfg, 0))
+    if eng._lora_rank:
+        ref.load_lora(synthetic_adapters(cfg, rank=eng._lora_rank))
+    ref.set_text_features(T.numpy(), SEGMENTS)
+    lr = ref.classify(px[:n]).logits.float()
+    lg = eng.classify(px[:n]).logits.float()
+    ref.close()
+    return float(((lg - lr).abs().amax(dim=1) / lr.abs().amax(dim=1)).max())
+
+
 def load_traffic(cfg_name: str, batch: int):
     """HBM bytes per launch of the dominant kernel from the rocprofv3 PMC passes of this bench
     command (tools/profile_round.sh -> profiles/pmc_traffic.json, which records the round it was
@@ -272,12 +286,19 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and a.lora_rank is not None:
-        bar = 2e-2 if a.dtype == "mxfp8" else 1e-3
         err = parity_check(eng, px, T, cfg)
-        line["parity"] = {"max_rel_logit_err_vs_cpu_fp32_oracle": round(err, 6), "images": 4, "bar": bar,
-                          "meets_bar": err <= bar,
-                          "note": "per image max|dlogit|/max|logit_ref| on the benched batch's first images"
-                                  + ("; mxfp8's bar is 2e-2 against the bf16 engine" if a.dtype == "mxfp8" else "")}
+        if a.dtype == "mxfp8":  # config 5: "logits within 2e-2 of bf16"
+            e16 = parity_vs_bf16(eng, px, T, cfg, dev)
+            line["parity"] = {"max_rel_logit_err_vs_bf16_engine": round(e16, 6), "images_vs_bf16": 64,
+                              "max_rel_logit_err_vs_cpu_fp32_oracle": round(err, 6), "images": 4, "bar": 2e-2,
+                              "meets_bar": e16 <= 2e-2,
+                              "note": "per image max|dlogit|/max|logit_ref|; the bar (BASELINE config 5) is "
+                                      "against the bf16 engine; logits of the bench's random unit text rows "
+                                      "(flat, max |logit| ~14): DESIGN.md 5.7 gives the CLIP-scale figure"}
+        else:
+            line["parity"] = {"max_rel_logit_err_vs_cpu_fp32_oracle": round(err, 6), "images": 4, "bar": 1e-3,
+                              "meets_bar": err <= 1e-3,
+                              "note": "per image max|dlogit|/max|logit_ref| on the benched batch's first images"}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(cfg, a.cpu_seconds)
     if rank == 0:
