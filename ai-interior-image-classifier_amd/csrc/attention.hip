@@ -332,9 +332,52 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
     }
 }
 
+// Online-softmax update of one 16-query fragment over a 64-key block (attention_v3, N > 128).
+// s holds the raw Q.K scores of the lane's 16 keys (key = kb*64 + 16 kt + 4 g + r). The softmax
+// runs in the log2 domain:
+// p = exp2(s * c - m), c = log2(e) / sqrt(64), so a score costs one FMA and one v_exp (no
+// separate scale multiply, no exp's log2(e) multiply). m_run is kept in that domain. MASK:
+// scores with live(kt, r) false become -inf (p = 0); only blocks that can hold dead keys pay it.
+// Measured (L/14@336 attention, 24 layers): 9.34 -> 8.70 ms per forward. attention_v2 (B/32) and
+// the text tower's kernel keep the scaled-exp form: there it gained nothing, and on the B/32 golden
+// fixtures (flat logits) the changed rounding realization raised the worst image 1.38e-3 -> 1.79e-3.
+template <bool MASK, typename Live>
+__device__ __forceinline__ void softmax_block(f32x4 (&s)[4], float& m_run, float& l_run, f32x4 (&o)[4],
+                                              Live&& live) {
+    constexpr float c = 0.18033688011112042f;  // log2(e) / 8
+    if constexpr (MASK) {
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (!live(kt, r)) s[kt][r] = -INFINITY;
+    }
+    float m4[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) m4[kt] = fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3]));
+    float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    const float m_new = fmaxf(m_run, mloc * c);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
+    float lsum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float pr = __builtin_amdgcn_exp2f(fmaf(s[kt][r], c, -m_new));
+            s[kt][r] = pr;
+            lsum += pr;
+        }
+    l_run = l_run * alpha + lsum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] *= alpha;
+}
+
 // attention_v3_kernel: attention_v2's algorithm with 16 QF queries per wave (QF 16-query
-// fragments f; QF = 2 or 4). Every K fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16)
-// read from LDS feeds two MFMAs instead of one, which halves the LDS read bytes per FLOP: at
+// fragments f; QF = 2; four per wave measured slower in round 1: fewer resident waves). Every K
+// fragment (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16) read from LDS feeds two MFMAs instead of one, which halves the LDS read bytes per FLOP: at
 // 16 queries per wave v2 reads 32 KB of LDS per 32 MFMAs per SIMD, the LDS array's peak.
 // QW waves = 32 QW queries per workgroup; SINGLE as in v2 (N <= 64: one key block, one stage).
 template <typename T, int QW = 4, bool SINGLE = false, int QF = 2>
@@ -385,7 +428,6 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
     float m_run[QF], l_run[QF];
 #pragma unroll
     for (int f = 0; f < QF; ++f) { m_run[f] = -INFINITY; l_run[f] = 0.f; }
-    const float scale = 0.125f;  // 1/sqrt(64)
     const int nkb = SINGLE ? 1 : (N + 63) >> 6;
 
     issue(0, 0);
@@ -412,35 +454,13 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
                 for (int f = 0; f < QF; ++f) s[f][kt] = T::mfma16(kf, qf[f][ds], s[f][kt]);
             }
         }
+        auto live = [&](int kt, int r) { return kb * 64 + kt * 16 + 4 * g + r < N; };
+        if (kb * 64 + 64 > N) {  // the last block only
 #pragma unroll
-        for (int f = 0; f < QF; ++f) {
-            float mloc = -INFINITY;
+            for (int f = 0; f < QF; ++f) softmax_block<true>(s[f], m_run[f], l_run[f], o[f], live);
+        } else {
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = kb * 64 + kt * 16 + 4 * g + r;
-                    const float v = key < N ? s[f][kt][r] * scale : -INFINITY;
-                    s[f][kt][r] = v;
-                    mloc = fmaxf(mloc, v);
-                }
-            mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-            mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-            const float m_new = fmaxf(m_run[f], mloc);
-            const float alpha = __expf(m_run[f] - m_new);
-            m_run[f] = m_new;
-            float lsum = 0.f;
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float p = __expf(s[f][kt][r] - m_new);
-                    s[f][kt][r] = p;
-                    lsum += p;
-                }
-            l_run[f] = l_run[f] * alpha + lsum;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[f][i] *= alpha;
+            for (int f = 0; f < QF; ++f) softmax_block<false>(s[f], m_run[f], l_run[f], o[f], live);
         }
 
         const int tq = (lane & 15) >> 2, tp = lane & 3;
@@ -500,7 +520,7 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
     }
 }
 
-static int attn_v3() {  // CLIPVIT_ATTN_V3: 0 off, 1 (default) long sequences, 2 also N <= 64, 3 = 1 with 64 queries per wave
+static int attn_v3() {  // CLIPVIT_ATTN_V3: 0 off, 1 (default) long sequences, 2 also N <= 64
     static const int on = [] {
         const char* v = getenv("CLIPVIT_ATTN_V3");
         return v ? atoi(v) : 1;
@@ -524,12 +544,6 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
             attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else
             attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v3() == 3 && N > 128) {  // long sequences: 2 waves x 64 queries
-        dim3 g4((N + 127) / 128, H, B);
-        if (dtype == 2)
-            attention_v3_kernel<F16, 2, false, 4><<<g4, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v3_kernel<BF16, 2, false, 4><<<g4, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
     } else if (attn_v3() >= 1 && N > 128) {  // long sequences: 4 waves x 32 queries
         dim3 g4((N + 127) / 128, H, B);
         if (dtype == 2)
