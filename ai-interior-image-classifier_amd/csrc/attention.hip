@@ -352,12 +352,10 @@ __device__ __forceinline__ void softmax_block(f32x4 (&s)[4], float& m_run, float
             for (int r = 0; r < 4; ++r)
                 if (!live(kt, r)) s[kt][r] = -INFINITY;
     }
-    float m4[4];
+    float mloc = fmaxf(s[0][0], s[0][1]);  // a chain the compiler folds into v_max3_f32
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) m4[kt] = fmaxf(fmaxf(s[kt][0], s[kt][1]), fmaxf(s[kt][2], s[kt][3]));
-    float mloc = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-    mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+    for (int i = 2; i < 16; ++i) mloc = fmaxf(mloc, s[i >> 2][i & 3]);
+    mloc = max_rows4(mloc);
     const float m_new = fmaxf(m_run, mloc * c);
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
     m_run = m_new;

@@ -41,10 +41,28 @@ struct F16 {
     }
 };
 
-// Pack two fp32 into one dword of two 16-bit values (lo first).
+// Pack two fp32 into one dword of two 16-bit values (lo first): one v_cvt_pk_{f16,bf16}_f32 (RNE,
+// the same rounding as two scalar conversions)
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 template <typename T>
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
-    return (unsigned)T::from_f32(lo) | ((unsigned)T::from_f32(hi) << 16);
+    if constexpr (__is_same(T, F16))
+        return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, f16x2_t));
+    else
+        return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){lo, hi}, bf16x2_t));
+}
+
+// max over the four lanes l, l ^ 16, l ^ 32, l ^ 48 (the 16-lane rows of a wave) by the gfx950
+// row-swap permutes (VALU; __shfl_xor is an LDS ds_bpermute round trip). Each swap exchanges
+// rows between its two operands; max of the two results is max(v[l], v[l ^ 16]) (resp. ^ 32)
+// in every lane, whichever operand received which half.
+__device__ __forceinline__ float max_rows4(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {
