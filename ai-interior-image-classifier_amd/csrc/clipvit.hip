@@ -136,12 +136,12 @@ struct clipvit_handle {
     std::mutex mu;
     std::vector<Workspace*> pool;
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from in-model sweeps on MI355X
-    // (tools/exp_sweep.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
+    // (tools/ab_env.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
     // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles). The 224x192
     // one-round tiles 92 / 93 win standalone (c_proj 67.4 -> 62.7 us, patch 75.2 -> 69.6) but
     // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158).
     // 98 = 240x256 QKV tiles of 12 waves (486 tiles = 1.9 rounds at bs 256 against 450 = 1.76
-    // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward (tools/exp_qkv240.sh)
+    // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward
     int var[5] = {98, 82, 13, 82, 22};
     bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
     int ncu = 256;            // compute units of the device
@@ -354,8 +354,9 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // [M1, M) on the role's small tile as a second launch. Row-wise independent outputs:
     // bit-identical to one launch. Measured (c_fc 12800 x 3072 x 768): 81.6 us in one launch
     // (128x128) or 77.6 (256x256, 3 rounds) -> 54.3 + 15.9 = 70.2 us.
-    // the main launch's tile: 256x256, or 256x192 for the 12-wave variants 69 / 89
-    const int bn = (h->split_main == 69 || h->split_main == 89) ? 192 : 256;
+    // the main launch's tile width: every pipelined variant a round split can use is 256 wide
+    // (8 / 80: 256x256, 98: 240x256)
+    const int bn = 256;
     if (h->round_split && !h->var_forced && (role == R_FC || role == R_QKV) && t256 &&
         N % bn == 0 && t256 < 4L * h->ncu &&
         (epi == EPI_STORE || epi == EPI_GELU || epi == EPI_LNF || epi == EPI_LNF_GELU)) {
@@ -846,8 +847,9 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_LNFOLD")) h->lnfold = h->resid16 && h->D <= 1024 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {
-        h->split_main = atoi(v);
+    if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
+        const int m = atoi(v);
+        if (m == 8 || m == 80) h->split_main = m;
         if (const char* c = strchr(v, ',')) h->split_tail = atoi(c + 1);
     }
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
