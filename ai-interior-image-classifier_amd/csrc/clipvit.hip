@@ -85,9 +85,15 @@ struct Lane {
 // by events), so one half's memory-bound kernels and GEMM tails overlap the other half's
 // GEMMs. Smaller batches run on the caller's stream with lane 0.
 constexpr int kLanes = 2;
-// Off by default: measured on MI355X, the half-batch GEMMs lose more to tile quantization
-// than the two lanes gain from overlapping (profiles/r01_*). CLIPVIT_SPLIT_MIN=n enables it.
+// Default: split batches of at least SPLIT_IMAGES images and SPLIT_TOKENS tokens (B/32: 256
+// images; B/16 and L/14@336: 128). Measured on MI355X (round 2, alternating A/B, same box):
+// B/32 bs 256 fp16 78.7k -> 80.8k and 78.2k -> 81.0k img/s on two boxes, 82.6k -> 82.1k on a
+// faster one; bf16 bs 512 81.5k -> 86.8k and 84.1k -> 87.0k; MX-fp8 bs 512 93.0k -> 99.0k;
+// L/14@336 bs 128 2,183 -> 2,269 and 2,179 -> 2,280; B/16 bs 256 21.25k -> 21.43k. Smaller
+// batches lose (B/32 bs 64 39.4k -> 38.2k, B/16 bs 64 20.3k -> 19.6k). Round 1 measured a loss
+// at bs 256 with the earlier tile table. CLIPVIT_SPLIT_MIN=n overrides (<= 0: never split).
 constexpr int SPLIT_NEVER = 1 << 30;
+constexpr int SPLIT_TOKENS = 12800, SPLIT_IMAGES = 128;
 struct Workspace {
     Lane lane[kLanes];
     hipEvent_t fork = nullptr;
@@ -147,7 +153,7 @@ struct clipvit_handle {
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid
     int xcd[5] = {2, 2, 2, 2, 1};
-    int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used
+    int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used (clipvit_create)
     // MX-fp8 mode (compute_dtype CLIPVIT_MXFP8): the four Linears of every block run as
     // MX-fp8 GEMMs (packed weight = N*Kp e4m3 bytes followed by N*Kp/32 E8M0 scales);
     // patch embedding, attention and everything else stay bf16 / fp32.
@@ -854,6 +860,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     }
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
     if (const char* v = getenv("CLIPVIT_MAX_INFLIGHT")) h->max_inflight = std::max(1, atoi(v));
+    h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);
     if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
         h->split_min = atoi(v);
         if (h->split_min <= 0) h->split_min = SPLIT_NEVER;

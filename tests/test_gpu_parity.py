@@ -133,7 +133,7 @@ def test_encode_image_unnormalised(gpu):
 
 
 def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
-    """The optional two-stream split (CLIPVIT_SPLIT_MIN) computes every image with the same
+    """The two-stream split (default from 12,800 tokens per batch; CLIPVIT_SPLIT_MIN) computes every image with the same
     kernels and k-order, so its outputs equal the single-stream outputs bit for bit."""
     cfg = C.VIT_B32
     sd = synthetic_state_dict(cfg, 0)
