@@ -1,13 +1,19 @@
 """Turn a tools/profile_round.sh output directory into committed summaries under profiles/.
 
-    python tools/summarize_profiles.py gpurun_out/prof r01
+    python tools/summarize_profiles.py gpurun_out/prof r02 [images_per_launch]
 writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim), profiles/<tag>_summary.md
 (per-kernel-role averages, MFMA TFLOP/s, PMC bytes per launch) and updates
 profiles/pmc_traffic.json (read by bench.py's roofline.traffic).
 
 Kernel roles are assigned from the dispatch order of one forward (per layer: qkv GEMM,
 attention, out GEMM, layernorm, fc GEMM, proj GEMM, layernorm), which is how out- and
-proj-GEMM dispatches of the same template instance are told apart.
+proj-GEMM dispatches of the same template instance are told apart. The order is followed per
+hardware queue: a batch split over the two lane streams interleaves two forwards in time.
+A dispatch is "isolated" when no dispatch of another queue overlaps it (bench.py's
+clipvit_profile_forward pass: one lane, serialised — what the bench's roofline times) and
+"concurrent" otherwise (the timed loop's two lanes share the GPU).
+
+images_per_launch: images per GEMM launch (bs 256 with the default two-lane split: 128).
 """
 import csv
 import json
@@ -85,62 +91,105 @@ def load_rows(path):
     return rows
 
 
+def roles_by_queue(rows, key="Start_Timestamp"):
+    """roles_for_trace applied to each hardware queue's dispatches in order."""
+    roles = [None] * len(rows)
+    byq = defaultdict(list)
+    for i, r in enumerate(rows):
+        byq[r.get("Queue_Id", "0")].append(i)
+    for idx in byq.values():
+        idx.sort(key=lambda i: int(rows[i][key]))
+        for i, role in zip(idx, roles_for_trace([rows[i] for i in idx])):
+            roles[i] = role
+    return roles
+
+
+def isolated_flags(rows):
+    """True for a dispatch that no dispatch of another queue overlaps in time."""
+    ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "0"), i)
+                 for i, r in enumerate(rows)))
+    iso = [True] * len(rows)
+    active = []  # (end, queue, index) of dispatches still running
+    for s0, e0, q, i in ev:
+        active = [a for a in active if a[0] > s0]
+        for e1, q1, j in active:
+            if q1 != q:
+                iso[i] = iso[j] = False
+        active.append((e0, q, i))
+    return iso
+
+
+def fc_split_rows(M, N=3072, ncu=256):
+    """Main-launch rows of clipvit.hip gemm()'s whole-round row split (0 = no split)."""
+    nN = N // 256
+    t256 = (M + 255) // 256 * nN
+    R, rem = divmod(t256, ncu)
+    m1 = R * ncu // nN * 256
+    return m1 if R >= 1 and 0 < rem and 2 * rem <= ncu and 0 < m1 < M else 0
+
+
 def main():
     src, tag = Path(sys.argv[1]), sys.argv[2]
+    lane_b = int(sys.argv[3]) if len(sys.argv) > 3 else 128
     prof = ROOT / "profiles"
     prof.mkdir(exist_ok=True)
     kt = next((src / "kt").rglob("*kernel_stats.csv"))
     shutil.copyfile(kt, prof / f"{tag}_kernel_stats.csv")
     trace = load_rows(next((src / "kt").rglob("*kernel_trace.csv")))
-    roles = roles_for_trace(trace)
-    dur = defaultdict(list)
-    for r, role in zip(trace, roles):
-        dur[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    roles = roles_by_queue(trace)
+    iso = isolated_flags(trace)
+    dur, dur_c = defaultdict(list), defaultdict(list)
+    for r, role, solo in zip(trace, roles, iso):
+        (dur if solo else dur_c)[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
     def pmc(kind):
         f = next((src / kind).rglob("*counter_collection.csv"))
         rows = [r for r in load_rows(f)]
-        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        rr = roles_for_trace(rows)
+        rr = roles_by_queue(rows, key="Dispatch_Id")
         acc = defaultdict(list)
         for r, role in zip(rows, rr):
             acc[role].append(float(r["Counter_Value"]))
         return acc
 
     fetch, write = pmc("fetch"), pmc("write")
-    M, D = 256 * 50, 768
-    # (rows, N, K) of each GEMM role at bs 256; c_fc with the whole-round row split: the main
-    # launch covers rows [0, 10752), the tail launch the other 2,048
-    shapes = {"qkv": (M, 3 * D, D), "out": (M, D, D), "proj": (M, D, 4 * D), "patch_gemm": (256 * 49, D, 3072)}
-    shapes["fc"] = (10752, 4 * D, D) if "fc_tail" in dur else (M, 4 * D, D)
-    if "fc_tail" in dur:
-        shapes["fc_tail"] = (M - 10752, 4 * D, D)
+    M, D = lane_b * 50, 768
+    # (rows, N, K) of each GEMM role per launch; c_fc with the whole-round row split: the main
+    # launch covers rows [0, m1), the tail launch the rest
+    shapes = {"qkv": (M, 3 * D, D), "out": (M, D, D), "proj": (M, D, 4 * D), "patch_gemm": (lane_b * 49, D, 3072)}
+    m1 = fc_split_rows(M)
+    shapes["fc"] = (m1, 4 * D, D) if m1 else (M, 4 * D, D)
+    if m1:
+        shapes["fc_tail"] = (M - m1, 4 * D, D)
     flops = {r: 2 * m * n * k for r, (m, n, k) in shapes.items()}
     # algorithmic bytes per launch: A once, W once, 16-bit C once
     algo = {r: 2 * (m * k + n * k + m * n) for r, (m, n, k) in shapes.items()}
-    lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16)", "",
-             "TFLOP/s = the launch's own FLOPs / rocprof average duration. Algorithmic MB = A + W + C",
-             "(16-bit) once. PMC MB = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction; L2 misses served",
-             "from the Infinity Cache are counted, writes still dirty in L2 at kernel end are not).", "",
-             "| role | dispatches | avg us | TFLOP/s | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic |",
-             "|---|---|---|---|---|---|---|---|"]
+    lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16; {lane_b} images per launch)", "",
+             "avg us / TFLOP/s: isolated dispatches (bench.py's serialised profile pass, what its roofline",
+             "times); concurrent us: the timed loop's dispatches, two lanes sharing the GPU. TFLOP/s = the",
+             "launch's own FLOPs / isolated average. Algorithmic MB = A + W + C (16-bit) once. PMC MB =",
+             "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction; L2 misses served from the Infinity Cache are",
+             "counted, writes still dirty in L2 at kernel end are not).", "",
+             "| role | isolated dispatches | avg us | TFLOP/s | concurrent avg us | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic |",
+             "|---|---|---|---|---|---|---|---|---|"]
     traffic = {}
-    for role in sorted(dur, key=lambda k: -sum(dur[k])):
-        d = dur[role]
+    for role in sorted(set(dur) | set(dur_c), key=lambda k: -sum(dur.get(k, [])) - sum(dur_c.get(k, []))):
+        d = dur.get(role) or dur_c[role]
         avg = sum(d) / len(d)
+        dc = dur_c.get(role, [])
+        cavg = f"{sum(dc) / len(dc):.1f}" if dc else ""
         tf = f"{flops[role] / (avg * 1e-6) / 1e12:.0f}" if role in flops else ""
         fb = 2 * sum(fetch[role]) / len(fetch[role]) * 1024 / 1e6 if fetch.get(role) else float("nan")
         wb = sum(write[role]) / len(write[role]) * 1024 / 1e6 if write.get(role) else float("nan")
         traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6}
         al = f"{algo[role] / 1e6:.1f}" if role in algo else ""
         ratio = f"{(fb + wb) * 1e6 / algo[role]:.2f}" if role in algo else ""
-        lines.append(f"| {role} | {len(d)} | {avg:.1f} | {tf} | {fb:.1f} | {wb:.1f} | {al} | {ratio} |")
+        lines.append(f"| {role} | {len(dur.get(role, []))} | {avg:.1f} | {tf} | {cavg} | {fb:.1f} | {wb:.1f} | {al} | {ratio} |")
     if "fc_tail" in traffic:  # one c_fc invocation = main + tail launch
         a, b = traffic["fc"], traffic.pop("fc_tail")
         traffic["fc"] = {k: a[k] + b[k] for k in a}
         t = traffic["fc"]
         fl, al = flops["fc"] + flops["fc_tail"], algo["fc"] + algo["fc_tail"]
-        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
+        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | | "
                      f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} | {al / 1e6:.1f} | "
                      f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
@@ -150,6 +199,7 @@ def main():
              "note": "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reports half of wide streaming reads); Infinity-Cache hits are included by the counters"}
     pj = prof / "pmc_traffic.json"
     data = json.loads(pj.read_text()) if pj.exists() else {}
+    entry["images_per_launch"] = lane_b
     data["ViT-B/32|256"] = entry
     pj.write_text(json.dumps(data, indent=1))
     print("\n".join(lines))
