@@ -85,15 +85,17 @@ struct Lane {
 // by events), so one half's memory-bound kernels and GEMM tails overlap the other half's
 // GEMMs. Smaller batches run on the caller's stream with lane 0.
 constexpr int kLanes = 2;
-// Default: split batches of at least SPLIT_IMAGES images and SPLIT_TOKENS tokens (B/32: 256
-// images; B/16 and L/14@336: 128). Measured on MI355X (round 2, alternating A/B, same box):
+// Default: split batches of at least SPLIT_IMAGES images and SPLIT_TOKENS tokens (B/32: 512
+// images; B/16 and L/14@336: 130 / 128). B/32 at bs 256 stays on one stream: there the split
+// won on some boxes and lost on others, and its half-batch launches make the per-kernel
+// roofline ill-defined. Measured on MI355X (round 2, alternating A/B, same box):
 // B/32 bs 256 fp16 78.7k -> 80.8k and 78.2k -> 81.0k img/s on two boxes, 82.6k -> 82.1k on a
 // faster one; bf16 bs 512 81.5k -> 86.8k and 84.1k -> 87.0k; MX-fp8 bs 512 93.0k -> 99.0k;
 // L/14@336 bs 128 2,183 -> 2,269 and 2,179 -> 2,280; B/16 bs 256 21.25k -> 21.43k. Smaller
 // batches lose (B/32 bs 64 39.4k -> 38.2k, B/16 bs 64 20.3k -> 19.6k). Round 1 measured a loss
 // at bs 256 with the earlier tile table. CLIPVIT_SPLIT_MIN=n overrides (<= 0: never split).
 constexpr int SPLIT_NEVER = 1 << 30;
-constexpr int SPLIT_TOKENS = 12800, SPLIT_IMAGES = 128;
+constexpr int SPLIT_TOKENS = 25600, SPLIT_IMAGES = 128;
 struct Workspace {
     Lane lane[kLanes];
     hipEvent_t fork = nullptr;
