@@ -68,10 +68,11 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("variant", STAGED)
+@pytest.mark.parametrize("variant", STAGED + (8, 13, 22))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
-    """LDS-staged row-contiguous 16-bit STORE / GELU epilogue on ragged M (last tile partial)."""
+    """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous
+    (80-82, 98) and direct from the accumulators (8: c_fc main launch and large-M c_fc; 13, 22)."""
     dtype = torch.float16
     M, N, K = 1000, 2304, 768
     if N % (256 if variant in N256 else 128):
