@@ -88,7 +88,7 @@ def lib() -> ctypes.CDLL:
             "clipvit_last_error": (ctypes.c_char_p, []),
             "clipvit_abi_version": (i, []),
             "clipvit_gemm_test": (i, [vp, i, vp, vp, vp, vp, i, i, i, i, i]),
-            "clipvit_attention_test": (i, [vp, i, vp, vp, i, i, i]),
+            "clipvit_attention_test": (i, [vp, i, vp, vp, i, i, i, i]),
             "clipvit_quant_mx8_test": (i, [vp, i, vp, i, i, vp, vp]),
             "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),

@@ -183,7 +183,9 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // per block (QW = 8 halves the K/V re-reads of long sequences: the fill path bounds them).
 // SINGLE (N <= 64, the B/32 shape): one key block, one LDS stage, no loop state — fewer live
 // registers, so more workgroups per CU hide the load latency.
-template <typename T, int QW = 4, bool SINGLE = false>
+// CAUSAL (text tower): key j masked for query i < j; key blocks past the workgroup's last query
+// are neither loaded nor computed.
+template <typename T, int QW = 4, bool SINGLE = false, bool CAUSAL = false>
 __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(const u16* __restrict__ qkv,
                                                                                 u16* __restrict__ out, int N, int H) {
     typedef typename T::vec8 vec8;
@@ -226,7 +228,8 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
     for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
     const float scale = 0.125f;  // 1/sqrt(64)
-    const int nkb = SINGLE ? 1 : (N + 63) >> 6;
+    int nkb = SINGLE ? 1 : (N + 63) >> 6;
+    if constexpr (CAUSAL) nkb = min(nkb, (min(N - 1, qb * (16 * QW) + 16 * QW - 1) >> 6) + 1);
 
     issue(0, 0);
     if (!SINGLE && nkb > 1) issue(1, 1);
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int key = kb * 64 + kt * 16 + 4 * g + r;
-                const float v = key < N ? s[kt][r] * scale : -INFINITY;
+                const float v = key < N && (!CAUSAL || key <= q) ? s[kt][r] * scale : -INFINITY;
                 s[kt][r] = v;
                 mloc = fmaxf(mloc, v);
             }
@@ -537,7 +540,12 @@ static bool attn_v2() {
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal) {
     dim3 grid((N + 63) / 64, H, B), block(256);
-    if (causal) {
+    if (causal && attn_v2()) {  // text tower: the glds-ring kernel with the causal mask
+        if (dtype == 2)
+            attention_v2_kernel<F16, 4, false, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        else
+            attention_v2_kernel<BF16, 4, false, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+    } else if (causal) {
         if (dtype == 2)
             attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
         else

@@ -1363,10 +1363,10 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
 }
 
 int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B, int N,
-                           int H) {
+                           int H, int causal) {
     g_err.clear();
     if (!qkv_dev || !out_dev || B <= 0 || N <= 0 || H <= 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
-    launch_attention((hipStream_t)stream, dtype, qkv_dev, out_dev, B, N, H);
+    launch_attention((hipStream_t)stream, dtype, qkv_dev, out_dev, B, N, H, causal != 0);
     HIPCHK(hipGetLastError());
     return 0;
 }

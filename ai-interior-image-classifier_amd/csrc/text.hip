@@ -114,6 +114,13 @@ struct clipvit_text_handle {
     float *x = nullptr, *eot = nullptr, *f = nullptr;
     void *h = nullptr, *qkv = nullptr, *u = nullptr;
     hipEvent_t done = nullptr;
+    // GEMM tiles (qkv, out, fc, proj; CLIPVIT_TEXT_VARIANTS="q,o,f,p") and the fp16 residual
+    // scheme of the vision tower (16-bit branch outputs + add_layernorm, deferred x store).
+    // Measured on the 437 label prompts (M = 33,649): fc on 128x128 (v13) 4.84 ms per call
+    // against 4.88-4.90 on 256x256 (v8: 1,056 tiles = 4.1 rounds); qkv 240x256 / 160x128 no
+    // better than 256x256; resid16 4.89 against 5.00 ms with the fp32 epilogue adds
+    int var[4] = {80, 82, 13, 82};
+    bool resid16 = false;
 };
 
 #define TFAIL(code, msg) \
@@ -159,8 +166,8 @@ static void text_pack(clipvit_text_handle* h, const std::string& name, void* dst
     launch_pack_weight(nullptr, h->dt, src ? src : h->master[name], dst, (int)sh[0], (int)sh[1], (int)sh[1]);
 }
 
-// variant: the vision roles' pipelined tiles (qkv / fc: 80 / 13, N = 512 roles: 82, 4x2 XCD
-// partition), falling back to the shape-based choice
+// variant: the vision roles' pipelined tiles (h->var; N = 512 roles with the 4x2 XCD partition),
+// falling back to the shape-based choice
 static int text_gemm(hipStream_t s, clipvit_text_handle* h, int epi, const void* A, const void* W,
                      const float* bias, void* C, int M, int N, int K, int variant) {
     GemmArgs a{};
@@ -210,6 +217,16 @@ int clipvit_text_create(const clipvit_text_config* cfg, int device, clipvit_text
     h->cfg = c;
     h->device = device;
     h->dt = c.compute_dtype;
+    h->resid16 = h->dt == CLIPVIT_F16;
+    if (const char* v = getenv("CLIPVIT_TEXT_RESID16")) h->resid16 = h->dt == CLIPVIT_F16 && atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_TEXT_VARIANTS")) {
+        int k = 0;
+        for (const char* q = v; *q && k < 4; ++k) {
+            h->var[k] = atoi(q);
+            while (*q && *q != ',') ++q;
+            if (*q == ',') ++q;
+        }
+    }
     *out = h;
     return 0;
 }
@@ -344,16 +361,37 @@ int clipvit_encode_text(clipvit_text_handle* h, void* stream, const int32_t* tok
     if (h->dt == CLIPVIT_F16) launch_text_embed<F16>(s, h, tokens_dev, M);
     else launch_text_embed<BF16>(s, h, tokens_dev, M);
     int rc = 0;
+    // fp16: out_proj / c_proj store their 16-bit branch outputs y, y2 into the qkv buffer (dead
+    // once attention has read it) and add_layernorm does the residual adds, x stored once per
+    // block ((x + y) + y2, the vision tower's deferred scheme, clipvit.hip forward()); the last
+    // block's c_proj adds into x in its epilogue (the EOT gather reads x). bf16: fp32 residual
+    // read-modify-write in the GEMM epilogues.
+    void* y = h->qkv;
+    void* y2 = (u16*)h->qkv + (size_t)M * D;
+    const int* v = h->var;
     for (int i = 0; i < h->cfg.layers && !rc; ++i) {
         const TextLayer& ly = h->layers[i];
-        if ((rc = text_gemm(s, h, EPI_STORE, h->h, ly.wqkv, ly.bqkv, h->qkv, M, 3 * D, D, 80))) break;
+        const bool last = i + 1 == h->cfg.layers;
+        if ((rc = text_gemm(s, h, EPI_STORE, h->h, ly.wqkv, ly.bqkv, h->qkv, M, 3 * D, D, v[0]))) break;
         launch_attention(s, h->dt, h->qkv, h->h, B, ctx, h->cfg.heads, /*causal=*/true);
-        if ((rc = text_gemm(s, h, EPI_RESID, h->h, ly.wout, ly.bout, h->x, M, D, D, 82))) break;
-        launch_layernorm(s, h->dt, h->x, h->h, ly.ln2g, ly.ln2b, M, D);
-        if ((rc = text_gemm(s, h, EPI_GELU, h->h, ly.wfc, ly.bfc, h->u, M, 4 * D, D, 13))) break;
-        if ((rc = text_gemm(s, h, EPI_RESID, h->u, ly.wproj, ly.bproj, h->x, M, D, 4 * D, 82))) break;
-        if (i + 1 < h->cfg.layers)
-            launch_layernorm(s, h->dt, h->x, h->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+        if (h->resid16) {
+            if ((rc = text_gemm(s, h, EPI_STORE, h->h, ly.wout, ly.bout, y, M, D, D, v[1]))) break;
+            if (last) launch_add_layernorm(s, h->dt, h->x, y, h->h, ly.ln2g, ly.ln2b, M, D);
+            else launch_add_layernorm_deferred(s, h->dt, h->x, y, nullptr, h->h, ly.ln2g, ly.ln2b, M, D);
+        } else {
+            if ((rc = text_gemm(s, h, EPI_RESID, h->h, ly.wout, ly.bout, h->x, M, D, D, v[1]))) break;
+            launch_layernorm(s, h->dt, h->x, h->h, ly.ln2g, ly.ln2b, M, D);
+        }
+        if ((rc = text_gemm(s, h, EPI_GELU, h->h, ly.wfc, ly.bfc, h->u, M, 4 * D, D, v[2]))) break;
+        if (h->resid16 && !last) {
+            if ((rc = text_gemm(s, h, EPI_STORE, h->u, ly.wproj, ly.bproj, y2, M, D, 4 * D, v[3]))) break;
+            const TextLayer& nx = h->layers[i + 1];
+            launch_add_layernorm_deferred(s, h->dt, h->x, y, y2, h->h, nx.ln1g, nx.ln1b, M, D);
+        } else {
+            if ((rc = text_gemm(s, h, EPI_RESID, h->u, ly.wproj, ly.bproj, h->x, M, D, 4 * D, v[3]))) break;
+            if (!last)
+                launch_layernorm(s, h->dt, h->x, h->h, h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, M, D);
+        }
     }
     if (!rc) {
         eot_gather_kernel<<<B, 64, 0, s>>>(tokens_dev, h->x, h->eot, ctx, D);

@@ -244,10 +244,10 @@ def gemm_mx8_test(A8: torch.Tensor, sA: torch.Tensor, W: torch.Tensor, bias: tor
     return (C, sC) if epi in (3, 4) else C
 
 
-def attention_test(qkv: torch.Tensor, B: int, N: int, H: int) -> torch.Tensor:
+def attention_test(qkv: torch.Tensor, B: int, N: int, H: int, causal: bool = False) -> torch.Tensor:
     L = _lib.lib()
     out = torch.empty((B * N, H * 64), dtype=qkv.dtype, device=qkv.device)
     with torch.cuda.device(qkv.device):
         s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
-        _lib.check(L.clipvit_attention_test(s, _DT[qkv.dtype], _vp(qkv), _vp(out), B, N, H))
+        _lib.check(L.clipvit_attention_test(s, _DT[qkv.dtype], _vp(qkv), _vp(out), B, N, H, int(causal)))
     return out

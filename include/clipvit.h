@@ -245,9 +245,9 @@ int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsig
                           unsigned char* sC_dev, int M, int N, int K, int epi, int variant);
 
 /* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
- * out [B*N, H*64] of `dtype`. */
+ * out [B*N, H*64] of `dtype`. causal != 0: key j masked for query i < j (the text tower). */
 int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B,
-                           int N, int H);
+                           int N, int H, int causal);
 
 /* Time `iters` launches of ONE lane's encoder forward (the per-stream batch the call path
  * launches for B images: ceil(B/2) when the batch is split over the two lane streams, else B)

@@ -143,11 +143,13 @@ def test_gemm_asymmetric_identity(gpu):
         assert torch.equal(C, W.to(torch.bfloat16).float().t()), variant
 
 
-def _ref_attention(qkv, B, N, H):
+def _ref_attention(qkv, B, N, H, causal=False):
     D = H * 64
     x = qkv.float().reshape(B, N, 3, H, 64)
     q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
     s = (q @ k.transpose(-1, -2)) / math.sqrt(64)
+    if causal:
+        s = s + torch.full((N, N), float("-inf"), device=s.device).triu(1)
     o = s.softmax(-1) @ v
     return o.transpose(1, 2).reshape(B * N, D)
 
@@ -160,6 +162,19 @@ def test_attention(gpu, dtype, tol, B, N, H):
     qkv = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).to(dtype)
     out = E.attention_test(qkv, B, N, H)
     ref = _ref_attention(qkv, B, N, H)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < tol, err
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2), (torch.float16, 3e-3)])
+@pytest.mark.parametrize("B,N,H", [(3, 77, 8), (2, 1, 8), (1, 64, 8), (2, 65, 8), (1, 200, 12)])
+def test_attention_causal(gpu, dtype, tol, B, N, H):
+    """The text tower's causal attention (CLIP.build_attention_mask: -inf above the diagonal)
+    against the fp32 reference, including blocks past the last query and single-token rows."""
+    g = torch.Generator(device=gpu).manual_seed(B * N * H + 1)
+    qkv = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).to(dtype)
+    out = E.attention_test(qkv, B, N, H, causal=True)
+    ref = _ref_attention(qkv, B, N, H, causal=True)
     err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < tol, err
 
