@@ -383,7 +383,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             c.C = (unsigned char*)C + (size_t)m1 * ldc * 2;
             if (c.st_in) c.st_in += (size_t)m1 * c.np;
             c.M = M - (int)m1;
-            c.xcd_n = 0;
+            c.xcd_n = h->xcd[role];  // tail: the role's partition (main: 1-D, whole rounds per XCD)
             if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 &&
                 launch_gemm(s, h->dt, epi, c, h->split_tail ? h->split_tail : variant) == 0)
                 return 0;
