@@ -193,8 +193,14 @@ __device__ __forceinline__ bool tile_of_block(int bid, int nM, int nN, int xn, i
     if (bid >= nwg) return false;
     const int q = nwg >> 3, r = nwg & 7, x = bid & 7;
     const int t = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
-    mt = t / nN;
-    nt = t % nN;
+    // xn = 32 + G (G | nN): the contiguous ranges follow a column-group-major order (G groups of
+    // nN / G N-tiles, M-rows inside a group), so an XCD group sweeps M with a 1/G share of W
+    // (small enough for its L2) instead of all of W
+    const int G = xn > 32 && nN % (xn - 32) == 0 ? xn - 32 : 1;
+    const int cg = nN / G, gsz = nM * cg;
+    const int g = t / gsz, rr = t - g * gsz;
+    mt = rr / cg;
+    nt = g * cg + rr % cg;
     return true;
 }
 

@@ -26,10 +26,11 @@ def _ref_gemm(A, W, bias, epi, C0=None):
     return ref
 
 
-# variant = 100 * xcd_partition + tile kernel (gemm.hip launch_t); 2xx = 4x2 XCD tile partition.
+# variant = 100 * xcd_partition + tile kernel (gemm.hip launch_t); 2xx = 4x2 XCD tile partition,
+# 34xx / 35xx = column-group-major 1-D remap with 2 / 3 N-groups (tile_of_block).
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 13 / 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail); 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 13, 22, 80, 81, 82, 90, 98, 208, 213, 222, 280, 282, 298]
+VARIANTS = [1, 2, 3, 8, 13, 22, 80, 81, 82, 90, 98, 208, 213, 222, 280, 282, 298, 3408, 3513, 3480]
 N128 = (1, 2, 13, 22, 81, 82)
 N256 = (3, 8, 80, 98)
 STAGED = (80, 81, 82, 98)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
