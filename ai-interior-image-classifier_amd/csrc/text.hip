@@ -217,8 +217,8 @@ int clipvit_text_create(const clipvit_text_config* cfg, int device, clipvit_text
     h->cfg = c;
     h->device = device;
     h->dt = c.compute_dtype;
-    h->resid16 = h->dt == CLIPVIT_F16;
-    if (const char* v = getenv("CLIPVIT_TEXT_RESID16")) h->resid16 = h->dt == CLIPVIT_F16 && atoi(v) != 0;
+    h->resid16 = true;  // both 16-bit types, as the vision tower
+    if (const char* v = getenv("CLIPVIT_TEXT_RESID16")) h->resid16 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_TEXT_VARIANTS")) {
         int k = 0;
         for (const char* q = v; *q && k < 4; ++k) {
@@ -361,11 +361,11 @@ int clipvit_encode_text(clipvit_text_handle* h, void* stream, const int32_t* tok
     if (h->dt == CLIPVIT_F16) launch_text_embed<F16>(s, h, tokens_dev, M);
     else launch_text_embed<BF16>(s, h, tokens_dev, M);
     int rc = 0;
-    // fp16: out_proj / c_proj store their 16-bit branch outputs y, y2 into the qkv buffer (dead
+    // resid16: out_proj / c_proj store their 16-bit branch outputs y, y2 into the qkv buffer (dead
     // once attention has read it) and add_layernorm does the residual adds, x stored once per
     // block ((x + y) + y2, the vision tower's deferred scheme, clipvit.hip forward()); the last
-    // block's c_proj adds into x in its epilogue (the EOT gather reads x). bf16: fp32 residual
-    // read-modify-write in the GEMM epilogues.
+    // block's c_proj adds into x in its epilogue (the EOT gather reads x). CLIPVIT_TEXT_RESID16=0:
+    // fp32 residual read-modify-write in the GEMM epilogues.
     void* y = h->qkv;
     void* y2 = (u16*)h->qkv + (size_t)M * D;
     const int* v = h->var;
