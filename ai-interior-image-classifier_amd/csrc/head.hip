@@ -22,6 +22,9 @@
 namespace clipvit {
 
 constexpr int HR = 16;     // images per workgroup
+constexpr int HW = 8;      // waves per workgroup (two per SIMD: one wave's LDS / global latency
+                           // hides behind the other's FMAs)
+constexpr int HT = 64 * HW;
 constexpr int HK = 128;    // reduction chunk (rows of the weight operand per LDS fill)
 constexpr int HMAXD = 20;  // max row length / 64 held in registers (width <= 1280)
 
@@ -33,15 +36,15 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
                                            int n, const float* __restrict__ gm,
                                            const float* __restrict__ bt, float* dst,
                                            float* __restrict__ norm_out) {
-    // the wave's HR / 4 rows: every load of every row is issued before the first reduction (one
+    // the wave's HR / HW rows: every load of every row is issued before the first reduction (one
     // memory round trip per wave instead of one per row)
-    constexpr int RW = HR / 4;
+    constexpr int RW = HR / HW;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nv = n >> 6;
     float v[RW][HMAXD];
 #pragma unroll
     for (int rr = 0; rr < RW; ++rr) {
-        const int b = min(b0 + wave + 4 * rr, B - 1);  // rows past B: clamped load, zero row below
+        const int b = min(b0 + wave + HW * rr, B - 1);  // rows past B: clamped load, zero row below
         const float* r = src + (size_t)b * stride;
 #pragma unroll
         for (int j = 0; j < HMAXD; ++j) {  // unconditional loads (clamped address), then select
@@ -51,7 +54,7 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
     }
 #pragma unroll
     for (int rr = 0; rr < RW; ++rr) {
-        const int i = wave + 4 * rr, b = b0 + i;
+        const int i = wave + HW * rr, b = b0 + i;
         float* d = dst + i * (n + 4);  // rows padded by 4 floats: the product's 4 image reads hit distinct banks
         if (b >= B) {
             for (int c = lane; c < n; c += 64) d[c] = 0.f;
@@ -92,50 +95,44 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
 // P = xs[16][K] @ W[K][col0 .. col0 + 64)  (K % 128 == 0), xs in LDS (row stride K + 4) staged
 // by `stage()`, which runs while the first two weight chunks are in flight. Weight chunks
 // (128 x 64) go global -> registers two chunks ahead of the multiply, registers -> LDS ws. Wave
-// w multiplies k-rows [32 w, 32 w + 32) of every chunk into a full 16 x 64 partial tile (lane:
-// images 4 (lane >> 4) .. + 3, columns 4 (lane & 15) .. + 3); the four partials are summed in a
-// fixed order at the end. On return red[i] holds output (image tid >> 4, columns 4 (tid & 15) + i).
+// w multiplies k-rows [16 w, 16 w + 16) of every chunk into a full 16 x 64 partial tile (lane:
+// images 4 (lane >> 4) .. + 3, columns 4 (lane & 15) .. + 3); the HW partials are summed in a
+// fixed order at the end. On return, threads tid < 256 hold in red[i] the output (image tid >> 4,
+// columns 4 (tid & 15) + i).
 template <typename Stage>
 __device__ __forceinline__ void tile_product(const float* xs, int K, const float* __restrict__ W, int ldw,
                                              int col0, float* ws, float (&red)[4], int tid, Stage&& stage) {
+    constexpr int KW = HK / HW;  // k-rows of a chunk per wave
     const int lane = tid & 63, wave = tid >> 6;
     const int ig = lane >> 4, cg = lane & 15;
-    const int lr = tid >> 4, lc = (tid & 15) * 4;
+    const int lr = tid >> 4, lc = (tid & 15) * 4;  // lr < HT / 16 = 32
     const int nc = K / HK;
     const int xstride = K + 4;
     float acc[4][4] = {};
-    // two register chunks of 8 float4 (named scalars: an array here ends up in scratch)
-    float4 a0, a1, a2, a3, a4, a5, a6, a7, b0, b1, b2, b3, b4, b5, b6, b7;
-    const size_t l16 = (size_t)16 * ldw;
-#define HEAD_LOAD(x0, x1, x2, x3, x4, x5, x6, x7, k0)                      \
+    // two register chunks of 4 float4 (named scalars: an array here ends up in scratch)
+    float4 a0, a1, a2, a3, b0, b1, b2, b3;
+    const size_t l32 = (size_t)32 * ldw;
+#define HEAD_LOAD(x0, x1, x2, x3, k0)                                      \
     {                                                                      \
         const float* p_ = W + (size_t)((k0) + lr) * ldw + col0 + lc;       \
         x0 = *(const float4*)p_;                                           \
-        x1 = *(const float4*)(p_ + l16);                                   \
-        x2 = *(const float4*)(p_ + 2 * l16);                               \
-        x3 = *(const float4*)(p_ + 3 * l16);                               \
-        x4 = *(const float4*)(p_ + 4 * l16);                               \
-        x5 = *(const float4*)(p_ + 5 * l16);                               \
-        x6 = *(const float4*)(p_ + 6 * l16);                               \
-        x7 = *(const float4*)(p_ + 7 * l16);                               \
+        x1 = *(const float4*)(p_ + l32);                                   \
+        x2 = *(const float4*)(p_ + 2 * l32);                               \
+        x3 = *(const float4*)(p_ + 3 * l32);                               \
     }
-#define HEAD_PUT(x0, x1, x2, x3, x4, x5, x6, x7)                           \
+#define HEAD_PUT(x0, x1, x2, x3)                                           \
     {                                                                      \
         float* q_ = ws + lr * 68 + lc;                                     \
         *(float4*)q_ = x0;                                                 \
-        *(float4*)(q_ + 16 * 68) = x1;                                     \
-        *(float4*)(q_ + 32 * 68) = x2;                                     \
-        *(float4*)(q_ + 48 * 68) = x3;                                     \
-        *(float4*)(q_ + 64 * 68) = x4;                                     \
-        *(float4*)(q_ + 80 * 68) = x5;                                     \
-        *(float4*)(q_ + 96 * 68) = x6;                                     \
-        *(float4*)(q_ + 112 * 68) = x7;                                    \
+        *(float4*)(q_ + 32 * 68) = x1;                                     \
+        *(float4*)(q_ + 64 * 68) = x2;                                     \
+        *(float4*)(q_ + 96 * 68) = x3;                                     \
     }
     auto mul = [&](int k0) {
-        const float* xr = xs + (4 * ig) * xstride + k0 + 32 * wave;
-        const float* wr = ws + (32 * wave) * 68 + 4 * cg;
-#pragma unroll 2
-        for (int k = 0; k < 32; k += 4) {
+        const float* xr = xs + (4 * ig) * xstride + k0 + KW * wave;
+        const float* wr = ws + (KW * wave) * 68 + 4 * cg;
+#pragma unroll
+        for (int k = 0; k < KW; k += 4) {
             float4 x[4], w[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = *(const float4*)(xr + i * xstride + k);
@@ -154,44 +151,44 @@ __device__ __forceinline__ void tile_product(const float* xs, int K, const float
             }
         }
     };
-    HEAD_LOAD(a0, a1, a2, a3, a4, a5, a6, a7, 0);
-    if (nc > 1) HEAD_LOAD(b0, b1, b2, b3, b4, b5, b6, b7, HK);
+    HEAD_LOAD(a0, a1, a2, a3, 0);
+    if (nc > 1) HEAD_LOAD(b0, b1, b2, b3, HK);
     stage();
     for (int c = 0; c < nc; c += 2) {
         __syncthreads();  // xs staged (first pass) / previous chunk's reads done
-        HEAD_PUT(a0, a1, a2, a3, a4, a5, a6, a7);
+        HEAD_PUT(a0, a1, a2, a3);
         __syncthreads();
-        if (c + 2 < nc) HEAD_LOAD(a0, a1, a2, a3, a4, a5, a6, a7, (c + 2) * HK);
+        if (c + 2 < nc) HEAD_LOAD(a0, a1, a2, a3, (c + 2) * HK);
         mul(c * HK);
         if (c + 1 >= nc) break;
         __syncthreads();
-        HEAD_PUT(b0, b1, b2, b3, b4, b5, b6, b7);
+        HEAD_PUT(b0, b1, b2, b3);
         __syncthreads();
-        if (c + 3 < nc) HEAD_LOAD(b0, b1, b2, b3, b4, b5, b6, b7, (c + 3) * HK);
+        if (c + 3 < nc) HEAD_LOAD(b0, b1, b2, b3, (c + 3) * HK);
         mul((c + 1) * HK);
     }
 #undef HEAD_LOAD
 #undef HEAD_PUT
-    // sum the four per-wave partial tiles (fixed order) through LDS
+    // sum the HW per-wave partial tiles (fixed order) through LDS
     __syncthreads();
-    float* part = ws;  // [4 waves][16 images][64 columns]
+    float* part = ws;  // [HW waves][16 images][64 columns]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
         *(float4*)(part + wave * 1024 + (4 * ig + i) * 64 + 4 * cg) =
             make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
     __syncthreads();
-    const int img = tid >> 4, cq = (tid & 15) * 4;
+    const int img = (tid & 255) >> 4, cq = (tid & 15) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[i] = 0.f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < HW; ++w) {
         const float4 v = *(const float4*)(part + w * 1024 + img * 64 + cq);
         red[0] += v.x; red[1] += v.y; red[2] += v.z; red[3] += v.w;
     }
 }
 
-// grid (ceil(B/16), E/64), 256 threads.
-__global__ __launch_bounds__(256) void cls_ln_proj_kernel(const float* __restrict__ x,
+// grid (ceil(B/16), E/64), HT threads.
+__global__ __launch_bounds__(HT) void cls_ln_proj_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ gm,
                                                           const float* __restrict__ bt,
                                                           const float* __restrict__ proj,
@@ -207,11 +204,12 @@ __global__ __launch_bounds__(256) void cls_ln_proj_kernel(const float* __restric
         stage_rows<0>(x, (size_t)N * D, b0, B, D, gm, bt, ys, nullptr);
     });
     const int b = b0 + (tid >> 4);
-    if (b < B) *(float4*)(f + (size_t)b * E + col0 + (tid & 15) * 4) = make_float4(red[0], red[1], red[2], red[3]);
+    if (tid < 256 && b < B)
+        *(float4*)(f + (size_t)b * E + col0 + (tid & 15) * 4) = make_float4(red[0], red[1], red[2], red[3]);
 }
 
-// grid (ceil(B/16), Cpad/64), 256 threads.
-__global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ f,
+// grid (ceil(B/16), Cpad/64), HT threads.
+__global__ __launch_bounds__(HT) void logits_kernel(const float* __restrict__ f,
                                                      const float* __restrict__ Tt,
                                                      float* __restrict__ emb_norm,
                                                      float* __restrict__ logits, int B, int E,
@@ -226,7 +224,7 @@ __global__ __launch_bounds__(256) void logits_kernel(const float* __restrict__ f
         stage_rows<1>(f, (size_t)E, b0, B, E, nullptr, nullptr, fs, blockIdx.y == 0 ? emb_norm : nullptr);
     });
     const int b = b0 + (tid >> 4), c = col0 + (tid & 15) * 4;
-    if (b < B) {
+    if (tid < 256 && b < B) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (c + i < C) logits[(size_t)b * C + c + i] = 100.0f * red[i];
@@ -294,7 +292,7 @@ void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const flo
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  160 * 1024) == hipSuccess;
     (void)attr;
-    dim3 grid((B + HR - 1) / HR, E / 64), block(256);
+    dim3 grid((B + HR - 1) / HR, E / 64), block(HT);
     const size_t lds = (HR * (D + 4) + HK * 68) * sizeof(float);
     cls_ln_proj_kernel<<<grid, block, lds, s>>>(x, g, b, proj, f, B, N, D, E);
 }
@@ -305,7 +303,7 @@ void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_no
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  160 * 1024) == hipSuccess;
     (void)attr;
-    dim3 grid((B + HR - 1) / HR, Cpad / 64), block(256);
+    dim3 grid((B + HR - 1) / HR, Cpad / 64), block(HT);
     const size_t lds = (HR * (E + 4) + HK * 68) * sizeof(float);
     logits_kernel<<<grid, block, lds, s>>>(f, Tt, emb_norm, logits, B, E, C, Cpad);
 }
