@@ -25,7 +25,6 @@
 namespace clipvit {
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ int mx_sw(int r) { return r & 7; }
 
@@ -383,287 +382,6 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_mx8_kernel(GemmArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// Wide MX tile on v_mfma_scale_f32_32x32x64_f8f6f4 (gemm_mx8w_kernel): 256-row tiles at half the
-// fragment registers per substep of the 16x16x128 form (a substep is 64 k deep instead of 128),
-// so a 128x64 wave tile double-buffers its fragments without spilling. Per k-step of 128 the
-// L2 -> LDS fill is the 16-bit 256x256 tile's bytes for twice its FLOPs.
-//  * operand lane map (tools/probes/mx32_probe.hip): lane l, r = l & 31, h = l >> 5, holds row r;
-//    bytes 0-15 belong to k-block 0 of the MFMA's 64 and bytes 16-31 to k-block 1 (any k order
-//    inside a block is fine as long as both operands use it). Here: substep s reads 16-B chunks
-//    4s + h (block 2s) and 4s + 2 + h (block 2s + 1) of the 128-B row. The scale of lane r + 32b
-//    applies to row r, block b: a lane passes its row's k-step scale dword shifted right by 8h
-//    and the MFMA's opsel picks byte 2s (= block 2s + h).
-//  * LDS rows are 128 B, chunk c of row r at c ^ mxw_sw(r): conflict-free ds_read_b128 for the
-//    32-row lane map (the 16x16 kernel's r & 7 would be 2-way).
-//  * output (swapped operands, D = W rows x tokens): lane (r, h) owns token r of a 32-token
-//    fragment and D rows (r' & 3) + 8 (r' >> 2) + 4h. With the 16-bit packer's 64-row weight
-//    permutation (launch_pack_weight_mx8, unchanged) the two 32-row W fragments of a 64-column
-//    wave tile give lane h the features 16h .. 16h+15 and 32 + 16h .. 32+16h+15: two runs of 16
-//    contiguous features, stored like the 16x16 kernel's one run; an MX block of 32 output
-//    features is lanes l and l ^ 32.
-__device__ __forceinline__ int mxw_sw(int r) { return (r & 7) ^ ((r >> 4) & 1); }
-
-template <typename TO, int BM, int BN, int WM, int WN, int EPI>
-__global__ __launch_bounds__(64 * WM* WN) void gemm_mx8w_kernel(GemmArgs a) {
-    constexpr int NT = 64 * WM * WN;
-    constexpr int TM = BM / WM, TN = BN / WN;
-    constexpr int FM = TM / 32, FN = TN / 32;
-    static_assert(TN % 64 == 0 && TM % 32 == 0, "wave tile: whole packed 64-row groups x 32k tokens");
-    constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128;
-    constexpr int LA = A_BYTES / (NT * 16), LW = W_BYTES / (NT * 16);
-    static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "whole staging rounds");
-    constexpr int SC_ROWS = BM + BN;
-    constexpr int SCL = (SC_ROWS + NT - 1) / NT;  // scale dwords per thread per k-step (row tid + r NT)
-    constexpr int STAGE = A_BYTES + W_BYTES + SCL * NT * 4;
-    __shared__ __attribute__((aligned(16))) unsigned char smem0[STAGE];
-    __shared__ __attribute__((aligned(16))) unsigned char smem1[STAGE];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave / WN, wn = wave % WN;
-    int mt, nt;
-    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, a.N / BN, a.xcd_n, mt, nt)) return;
-    const int m0 = mt * BM, n0 = nt * BN;
-
-    const unsigned char* Ab = (const unsigned char*)a.A;
-    const unsigned char* Wb = (const unsigned char*)a.W;
-    const size_t ldb = (size_t)a.K;
-    const size_t lds_ = (size_t)(a.K / 32);
-    const int mlast = a.M - 1;
-    unsigned asrc[LA], wsrc[LW];
-#pragma unroll
-    for (int r = 0; r < LA; ++r) {
-        const int p = r * NT * 16 + tid * 16;
-        const int row = p >> 7, c = ((p >> 4) & 7) ^ mxw_sw(row);
-        asrc[r] = (unsigned)((size_t)min(m0 + row, mlast) * ldb + c * 16);
-    }
-#pragma unroll
-    for (int r = 0; r < LW; ++r) {
-        const int p = r * NT * 16 + tid * 16;
-        const int row = p >> 7, c = ((p >> 4) & 7) ^ mxw_sw(row);
-        wsrc[r] = (unsigned)((size_t)(n0 + row) * ldb + c * 16);
-    }
-    const unsigned char* ssrc[SCL];  // row t: A rows first, then W rows; t >= SC_ROWS: pad
-#pragma unroll
-    for (int r = 0; r < SCL; ++r) {
-        const int t = r * NT + tid;
-        ssrc[r] = t < BM ? a.sA + (size_t)min(m0 + t, mlast) * lds_
-                : t < SC_ROWS ? a.sW + (size_t)(n0 + t - BM) * lds_ : a.sW + (size_t)n0 * lds_;
-    }
-    auto stage = [&](auto B, int kt) {
-        unsigned char* sA = decltype(B)::value ? smem1 : smem0;
-        unsigned char* sW = sA + A_BYTES;
-        unsigned char* sS = sW + W_BYTES;
-        const unsigned kofs = (unsigned)kt * 128;
-#pragma unroll
-        for (int r = 0; r < LA; ++r) glds16(Ab + (asrc[r] + kofs), sA + r * NT * 16 + wave * 1024);
-#pragma unroll
-        for (int r = 0; r < LW; ++r) glds16(Wb + (wsrc[r] + kofs), sW + r * NT * 16 + wave * 1024);
-#pragma unroll
-        for (int r = 0; r < SCL; ++r)
-            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(ssrc[r] + kt * 4),
-                                             (LDS_AS void*)(sS + r * NT * 4 + wave * 256), 4, 0, 0);
-    };
-
-    const int lr = lane & 31, lh = lane >> 5;
-    const int fsw = mxw_sw(lr);
-    // chunk byte offsets of substep s: lo = chunk 4s + h, hi = chunk 4s + 2 + h
-    const int cl0 = (lh ^ fsw) << 4, ch0 = ((2 + lh) ^ fsw) << 4;
-    const int cl1 = ((4 + lh) ^ fsw) << 4, ch1 = ((6 + lh) ^ fsw) << 4;
-    const int fa = (wm * TM + lr) * 128;
-    const int fw = A_BYTES + (wn * TN + lr) * 128;
-    const int fsa = A_BYTES + W_BYTES + (wm * TM + lr) * 4;
-    const int fsw4 = A_BYTES + W_BYTES + (BM + wn * TN + lr) * 4;
-    const int shift = 8 * lh;
-    auto frag = [&](const unsigned char* p, int s) -> i32x8 {
-        const uint4 lo = *(const uint4*)(p + (s ? cl1 : cl0));
-        const uint4 hi = *(const uint4*)(p + (s ? ch1 : ch0));
-        return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
-    };
-    auto fragA = [&](auto B, int s, int fm) -> i32x8 {
-        return frag((decltype(B)::value ? smem1 : smem0) + fa + fm * 4096, s);
-    };
-    auto fragW = [&](auto B, int s, int fn) -> i32x8 {
-        return frag((decltype(B)::value ? smem1 : smem0) + fw + fn * 4096, s);
-    };
-    auto load_scales = [&](auto B, int (&as)[FM], int (&ws)[FN]) {
-        const unsigned char* sb = decltype(B)::value ? smem1 : smem0;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) ws[fn] = *(const int*)(sb + fsw4 + fn * 128) >> shift;
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) as[fm] = *(const int*)(sb + fsa + fm * 128) >> shift;
-    };
-
-    f32x16 acc[FN][FM];
-#pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-        for (int j = 0; j < FM; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    // Registers: one set of A fragments, re-read in place right after its last MFMA; W
-    // fragments double-buffered (wf current, wx next). A substep (k-step kt, half s) runs
-    // FN x FM MFMAs (opsel 2s picks block 2s + h of the shifted scale dwords) while the next
-    // substep's fragments are read from stage NB, half NS.
-    i32x8 af[FM], wf[FN], wx[FN];
-    int sa0[FM], sw0[FN], sa1[FM], sw1[FN];
-    auto sub = [&](auto S, auto NB, auto NS, const int (&as)[FM], const int (&ws)[FN]) {
-        constexpr int os = 2 * decltype(S)::value;
-        constexpr int ns = decltype(NS)::value;
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) wx[fn] = fragW(NB, ns, fn);
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) {
-#pragma unroll
-            for (int fn = 0; fn < FN; ++fn)
-                acc[fn][fm] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[fn], af[fm], acc[fn][fm], 0, 0, os,
-                                                                               ws[fn], os, as[fm]);
-            af[fm] = fragA(NB, ns, fm);
-        }
-        // order: the W reads, then per A fragment its FN MFMAs followed by its two reads
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * FN, 0);
-#pragma unroll
-        for (int fm = 0; fm < FM; ++fm) {
-            __builtin_amdgcn_sched_group_barrier(0x008, FN, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn) wf[fn] = wx[fn];
-    };
-
-    const int nk = a.K >> 7;
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    stage(P0{}, 0);
-    vm_wait<0>();
-    __builtin_amdgcn_s_barrier();
-    if (nk > 1) stage(P1{}, 1);
-#pragma unroll
-    for (int fn = 0; fn < FN; ++fn) wf[fn] = fragW(P0{}, 0, fn);
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm) af[fm] = fragA(P0{}, 0, fm);
-    load_scales(P0{}, sa0, sw0);
-
-    // k-step kt with a successor: substep 0 reads substep 1's fragments (same stage); after the
-    // barrier that hands over stage kt+1, substep 1 reads the next k-step's substep-0 fragments
-    // and scales from stage kt+1
-    auto kstep = [&](int kt, auto P, int (&sac)[FM], int (&swc)[FN], int (&san)[FM], int (&swn)[FN]) {
-        constexpr int cur = decltype(P)::value;
-        using PN = std::integral_constant<int, cur ^ 1>;
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        sub(P0{}, P, P1{}, sac, swc);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // stage kt fully read
-        vm_wait<0>();                        // stage kt+1 landed (own loads)
-        __builtin_amdgcn_s_barrier();
-        stage(P, min(kt + 2, nk - 1));       // branch-free refill (past the end: an unused k-step)
-        load_scales(PN{}, san, swn);
-        sub(P1{}, PN{}, P0{}, sac, swc);
-    };
-    auto klast = [&](auto P, int (&sac)[FM], int (&swc)[FN]) {
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        sub(P0{}, P, P1{}, sac, swc);
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-#pragma unroll
-        for (int fn = 0; fn < FN; ++fn)
-#pragma unroll
-            for (int fm = 0; fm < FM; ++fm)
-                acc[fn][fm] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(wf[fn], af[fm], acc[fn][fm], 0, 0, 2,
-                                                                               swc[fn], 2, sac[fm]);
-    };
-    int kt = 0;
-    for (; kt + 2 < nk; kt += 2) {
-        kstep(kt, P0{}, sa0, sw0, sa1, sw1);
-        kstep(kt + 1, P1{}, sa1, sw1, sa0, sw0);
-    }
-    if (kt + 2 == nk) {
-        kstep(kt, P0{}, sa0, sw0, sa1, sw1);
-        klast(P1{}, sa1, sw1);
-    } else {
-        klast(P0{}, sa0, sw0);
-    }
-
-    // ---- epilogue: lane (lr, lh) owns token m and, per 64-group q and run R, features n .. n+15 ----
-#pragma unroll
-    for (int fm = 0; fm < FM; ++fm) {
-        const int m = m0 + wm * TM + fm * 32 + lr;
-#pragma unroll
-        for (int qr = 0; qr < TN / 32; ++qr) {
-            const int q = qr >> 1, R = qr & 1;
-            const int n = n0 + wn * TN + 64 * q + 32 * R + 16 * lh;
-            float v[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = acc[2 * q + (j >> 3)][fm][(j & 3) + 4 * R + 8 * ((j >> 2) & 1)];
-            if (a.bias) {
-                const float4* b4 = (const float4*)(a.bias + n);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float4 bb = b4[i];
-                    v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
-                }
-            }
-            if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_F32GELU) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
-            }
-            if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_Q8) {
-                float am = 0.f;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) am = fmaxf(am, fabsf(v[i]));
-                am = fmaxf(am, __shfl_xor(am, 32, 64));
-                if (m >= a.M) continue;
-                const int e = mx_exp(am);
-                const float inv = mx_inv(e);
-                *(uint4*)((unsigned char*)a.C + (size_t)m * a.ldc + n) =
-                    make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
-                               pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
-                               pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
-                               pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
-                if (lh == 0) a.sC[(size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
-                continue;
-            }
-            if (m >= a.M) continue;
-            if constexpr (EPI == EPI_STORE) {
-                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
-                dst[0] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                                    pack2<TO>(v[6], v[7]));
-                dst[1] = make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]),
-                                    pack2<TO>(v[12], v[13]), pack2<TO>(v[14], v[15]));
-            } else if constexpr (EPI == EPI_RESID) {
-                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float4 o = dst[i];
-                    o.x += v[4 * i]; o.y += v[4 * i + 1]; o.z += v[4 * i + 2]; o.w += v[4 * i + 3];
-                    dst[i] = o;
-                }
-            } else {  // EPI_F32 / EPI_F32GELU
-                float4* dst = (float4*)((float*)a.C + (size_t)m * a.ldc + n);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) dst[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-            }
-        }
-    }
-}
-
-template <typename TO, int BM, int BN, int WM, int WN>
-static int launch_mx8w_tile(hipStream_t s, int epi, const GemmArgs& a) {
-    if (a.N % BN) return -1;
-    const int nwg = grid_for((a.M + BM - 1) / BM, a.N / BN, a.xcd_n);
-    dim3 grid(nwg), block(64 * WM * WN);
-    switch (epi) {
-        case EPI_STORE: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_STORE><<<grid, block, 0, s>>>(a); break;
-        case EPI_RESID: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_RESID><<<grid, block, 0, s>>>(a); break;
-        case EPI_GELU_Q8: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_GELU_Q8><<<grid, block, 0, s>>>(a); break;
-        case EPI_Q8: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_Q8><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_F32><<<grid, block, 0, s>>>(a); break;
-        case EPI_F32GELU: gemm_mx8w_kernel<TO, BM, BN, WM, WN, EPI_F32GELU><<<grid, block, 0, s>>>(a); break;
-        default: return -1;
-    }
-    return 0;
-}
-
 template <typename TO, int BM, int BN, int WM, int WN>
 static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
     if (a.N % BN) return -1;
@@ -681,16 +399,13 @@ static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
     return 0;
 }
 
-// variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves); 16x16x128 MFMA.
-// 3 256x256 (2x4 waves), 4 256x128 (4x2 waves); 32x32x64 MFMA (gemm_mx8w_kernel)
+// variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves)
 template <typename TO>
 static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
     if (variant == 0) variant = a.N % 256 == 0 ? 1 : 2;
     switch (variant) {
         case 1: return launch_mx8_tile<TO, 128, 256, 2, 4>(s, epi, a);
         case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
-        case 3: return launch_mx8w_tile<TO, 256, 256, 2, 4>(s, epi, a);  // 32x32x64 MFMA
-        case 4: return launch_mx8w_tile<TO, 256, 128, 4, 2>(s, epi, a);
     }
     return -1;
 }

@@ -96,14 +96,12 @@ def _quantized_operands(gpu, M, N, K, seed):
     return A8, sA, W.to(gpu), bias.to(gpu), _dequant(A8, sA), _dequant(W8, sW)
 
 
-# 1 / 2: 128x256 / 128x128 on the 16x16x128 scaled MFMA; 3 / 4: 256x256 / 256x128 on the
-# 32x32x64 one (gemm_mx8w_kernel); 2xx = 4x2 XCD tile partition, 34xx = column-group-major
-@pytest.mark.parametrize("variant", [1, 2, 201, 3, 4, 203, 3403])
+@pytest.mark.parametrize("variant", [1, 2, 201])
 @pytest.mark.parametrize("M,N,K", [(12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
-                                   (700, 768, 3072), (64, 256, 128), (130, 128, 256), (300, 512, 384)])
+                                   (700, 768, 3072), (64, 256, 128), (130, 128, 256)])
 def test_gemm_mx8_vs_dequantized_reference(gpu, variant, M, N, K):
-    if variant % 100 in (1, 3) and N % 256:
-        pytest.skip("256-wide tile needs N % 256 == 0")
+    if variant % 100 == 1 and N % 256:
+        pytest.skip("128x256 tile needs N % 256 == 0")
     A8, sA, W, bias, Ad, Wd = _quantized_operands(gpu, M, N, K, M + N + K)
     Cg = E.gemm_mx8_test(A8, sA, W, bias, epi=0, variant=variant).cpu().numpy()
     ref = Ad @ Wd.T + bias.cpu().numpy()[None, :]
@@ -119,33 +117,30 @@ def test_gemm_mx8_exact_integers(gpu):
     W = torch.randint(-3, 4, (N, K), generator=g).float()
     W[:, ::7] = 0
     A8, sA = E.quant_mx8_test(A.to(gpu))
-    for variant in (1, 2, 3, 4):
+    for variant in (1, 2):
         Cg = E.gemm_mx8_test(A8, sA, W.to(gpu), None, epi=0, variant=variant).cpu()
         assert torch.equal(Cg, A @ W.t()), variant
 
 
-@pytest.mark.parametrize("variant", [0, 3, 4])
-def test_gemm_mx8_epilogues(gpu, variant):
-    """Every epilogue on ragged M; the MX-fp8 outputs (an MX block = two lanes' 16 features)
-    must equal the quantization of the same tile's fp32 outputs."""
+def test_gemm_mx8_epilogues(gpu):
     M, N, K = 515, 1024, 768
     A8, sA, W, bias, Ad, Wd = _quantized_operands(gpu, M, N, K, 21)
-    c0 = E.gemm_mx8_test(A8, sA, W, bias, epi=0, variant=variant)
-    c1 = E.gemm_mx8_test(A8, sA, W, bias, epi=1, variant=variant)
+    c0 = E.gemm_mx8_test(A8, sA, W, bias, epi=0)
+    c1 = E.gemm_mx8_test(A8, sA, W, bias, epi=1)
     ref = torch.from_numpy(Ad @ Wd.T).float() + bias.cpu()[None, :]
     gelu = ref * torch.sigmoid(1.702 * ref)
     assert ((c1.cpu() - gelu).abs().max() / gelu.abs().max()).item() < 1e-4
     # residual accumulate
     x0 = torch.randn(M, N, device=gpu)
-    c2 = E.gemm_mx8_test(A8, sA, W, bias, epi=2, C=x0.clone(), variant=variant)
+    c2 = E.gemm_mx8_test(A8, sA, W, bias, epi=2, C=x0.clone())
     assert torch.allclose(c2, x0 + c0, rtol=0, atol=1e-5 * (x0 + c0).abs().max().item())
     # MX-fp8 outputs = quantization of the fp32 ones (same kernel arithmetic)
     for epi, base in ((3, c0), (4, c1)):
-        q, s = E.gemm_mx8_test(A8, sA, W, bias, epi=epi, variant=variant)
+        q, s = E.gemm_mx8_test(A8, sA, W, bias, epi=epi)
         q_ref, s_ref = E.quant_mx8_test(base)
         assert torch.equal(s, s_ref) and torch.equal(q, q_ref), epi
     # bf16 store
-    c5 = E.gemm_mx8_test(A8, sA, W, bias, epi=5, variant=variant)
+    c5 = E.gemm_mx8_test(A8, sA, W, bias, epi=5)
     assert torch.equal(c5, c0.to(torch.bfloat16))
 
 
