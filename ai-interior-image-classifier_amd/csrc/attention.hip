@@ -209,17 +209,21 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
 
     // glds assignment: wave w fills key rows [RW w, RW w + RW) of K and of V (1 KB pieces)
     constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
+    // K/V staging by buffer loads over this image's rows: per-lane offsets constant over the key
+    // blocks, the block's offset in an SGPR; key rows >= N lie past the resource's range and read
+    // as zeros (their scores are masked, and P = 0 there)
     const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
+    const i32x4_t rs = buf_rsrc(src, (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128));
     auto issue = [&](int kb, int st) {
         unsigned char* dst = smem + st * STAGE;
+        const int kofs = kb * 64 * ld * 2;
 #pragma unroll
         for (int r = 0; r < RW / 8; ++r) {
             const int row = wave * RW + r * 8 + (lane >> 3);
-            const int key = min(kb * 64 + row, N - 1);
             const int c = (lane & 7) ^ (row & 7);
-            const unsigned char* ks = src + (size_t)key * ld * 2 + c * 16;
-            glds16(ks, dst + (wave * RW + r * 8) * 128);
-            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * RW + r * 8) * 128);
+            const unsigned off = (unsigned)(row * ld * 2 + c * 16);
+            blds16(rs, off, kofs, dst + (wave * RW + r * 8) * 128);
+            blds16(rs, off + (unsigned)D * 2, kofs, dst + 8192 + (wave * RW + r * 8) * 128);
         }
     };
 
@@ -407,17 +411,21 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
     }
 
     constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
+    // K/V staging by buffer loads over this image's rows: per-lane offsets constant over the key
+    // blocks, the block's offset in an SGPR; key rows >= N lie past the resource's range and read
+    // as zeros (their scores are masked, and P = 0 there)
     const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
+    const i32x4_t rs = buf_rsrc(src, (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128));
     auto issue = [&](int kb, int st) {
         unsigned char* dst = smem + st * STAGE;
+        const int kofs = kb * 64 * ld * 2;
 #pragma unroll
         for (int r = 0; r < RW / 8; ++r) {
             const int row = wave * RW + r * 8 + (lane >> 3);
-            const int key = min(kb * 64 + row, N - 1);
             const int c = (lane & 7) ^ (row & 7);
-            const unsigned char* ks = src + (size_t)key * ld * 2 + c * 16;
-            glds16(ks, dst + (wave * RW + r * 8) * 128);
-            glds16(ks + (size_t)D * 2, dst + 8192 + (wave * RW + r * 8) * 128);
+            const unsigned off = (unsigned)(row * ld * 2 + c * 16);
+            blds16(rs, off, kofs, dst + (wave * RW + r * 8) * 128);
+            blds16(rs, off + (unsigned)D * 2, kofs, dst + 8192 + (wave * RW + r * 8) * 128);
         }
     };
 

@@ -83,6 +83,26 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
                                      0);
 }
 
+// 16-byte async copy through a buffer resource -> LDS (buffer_load_dwordx4 ... offen lds):
+// per-lane 32-bit byte offset voff (a VGPR that can stay constant across k-steps), wave-uniform
+// soff (SGPR: the k offset), range-checked against the resource's byte count.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ void raw_buffer_load_lds(i32x4_t rsrc, LDS_AS void* lds, int size, int voffset, int soffset, int offset,
+                                    int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+// raw (stride 0) buffer resource over [base, base + bytes); base and bytes wave-uniform
+__device__ __forceinline__ i32x4_t buf_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long pa = (unsigned long long)base;
+    i32x4_t r;
+    r.x = (int)(unsigned)pa;
+    r.y = (int)((unsigned)(pa >> 32) & 0xffffu);
+    r.z = (int)bytes;
+    r.w = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle
+    return r;
+}
+__device__ __forceinline__ void blds16(i32x4_t rsrc, unsigned voff, int soff, void* lds_wave_base) {
+    raw_buffer_load_lds(rsrc, (LDS_AS void*)lds_wave_base, 16, (int)voff, soff, 0, 0);
+}
+
 // ---- MX-fp8: OCP e4m3 elements, one E8M0 (power-of-two) scale per 32 consecutive K ----
 // Block rule (shared by every producer and by the tests' host reference): e = the smallest
 // integer with amax * 2^-e <= 448 (e4m3's largest finite), clamped to [-127, 126]; scale byte

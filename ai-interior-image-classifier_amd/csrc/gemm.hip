@@ -379,10 +379,36 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
     // split-K slice (EPI_F32 only, launch_pipe): k-tiles [kz * nk, kz * nk + nk) of the row
     const int kz = a.ksplit > 1 ? (int)blockIdx.y : 0;
     const size_t kbase = a.ksplit > 1 ? (size_t)kz * (a.K / a.ksplit) * 2 : 0;
+    // Staging by buffer loads over the tile's own rows (resource base = first row of the tile):
+    // the 32-bit per-lane offsets stay constant over k and the k offset is an SGPR, so a k-step
+    // issues no address arithmetic (global_load_lds needed a 64-bit add per piece; measured
+    // B/32 bs 256 83.3k -> 83.9k img/s, c_proj 0.739 -> 0.723 ms per forward). The implicit-GEMM
+    // patch path keeps per-lane global addresses (its k offset is not separable).
+    constexpr bool BUFL = PIMPL == 0;
+    i32x4_t rsA{}, rsW{};
+    unsigned boa[BUFL ? LA : 1], bow[BUFL ? LW : 1];
+    if constexpr (BUFL) {
+        const size_t abytes = (size_t)(a.M - m0) * ldb, wbytes = (size_t)(a.N - n0) * ldb;
+        rsA = buf_rsrc(Ab + (size_t)m0 * ldb, (unsigned)min(abytes, (size_t)0xFFFFFFFFu));
+        rsW = buf_rsrc(Wb + (size_t)n0 * ldb, (unsigned)min(wbytes, (size_t)0xFFFFFFFFu));
+#pragma unroll
+        for (int r = 0; r < LA; ++r) boa[r] = (unsigned)(asrc[r] - (size_t)m0 * ldb);
+#pragma unroll
+        for (int r = 0; r < LW; ++r) bow[r] = (unsigned)(wsrc[r] - (size_t)n0 * ldb);
+    }
     auto stage = [&](int buf, int kt) {
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = kbase + (size_t)kt * 128;
+        if constexpr (BUFL) {
+#pragma unroll
+            for (int r = 0; r < LA; ++r)
+                if (r * NT * 16 + wave * 1024 < A_BYTES) blds16(rsA, boa[r], (int)kofs, sA + r * NT * 16 + wave * 1024);
+#pragma unroll
+            for (int r = 0; r < LW; ++r)
+                if (r * NT * 16 + wave * 1024 < W_BYTES) blds16(rsW, bow[r], (int)kofs, sW + r * NT * 16 + wave * 1024);
+            return;
+        }
 #pragma unroll
         for (int r = 0; r < LA; ++r)
             if (r * NT * 16 + wave * 1024 < A_BYTES) {  // wave-uniform

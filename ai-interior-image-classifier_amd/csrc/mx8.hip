@@ -188,15 +188,19 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_mx8_kernel(GemmArgs a) {
                               : tid < SC_ROWS ? a.sW + (size_t)(n0 + tid - BM) * lds_
                                               : a.sW + (size_t)n0 * lds_;
 
+    // operand staging by buffer loads: constant 32-bit per-lane offsets, k offset in an SGPR
+    // (same scheme as gemm_pipe_kernel)
+    const i32x4_t rsA = buf_rsrc(Ab, (unsigned)min((size_t)a.M * ldb, (size_t)0xFFFFFFFFu));
+    const i32x4_t rsW = buf_rsrc(Wb, (unsigned)min((size_t)a.N * ldb, (size_t)0xFFFFFFFFu));
     auto stage = [&](auto B, int kt) {
         unsigned char* sA = decltype(B)::value ? smem1 : smem0;
         unsigned char* sW = sA + A_BYTES;
         unsigned char* sS = sW + W_BYTES;
-        const unsigned kofs = (unsigned)kt * 128;
+        const int kofs = kt * 128;
 #pragma unroll
-        for (int r = 0; r < LA; ++r) glds16(Ab + (asrc[r] + kofs), sA + r * NT * 16 + wave * 1024);
+        for (int r = 0; r < LA; ++r) blds16(rsA, asrc[r], kofs, sA + r * NT * 16 + wave * 1024);
 #pragma unroll
-        for (int r = 0; r < LW; ++r) glds16(Wb + (wsrc[r] + kofs), sW + r * NT * 16 + wave * 1024);
+        for (int r = 0; r < LW; ++r) blds16(rsW, wsrc[r], kofs, sW + r * NT * 16 + wave * 1024);
         __builtin_amdgcn_global_load_lds((const GLB_AS void*)(ssrc + kt * 4),
                                          (LDS_AS void*)(sS + wave * 256), 4, 0, 0);
     };
