@@ -8,10 +8,12 @@ load, every entry point raises ``ClipVitError``.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libclipvit_hip.so"
+# CLIPVIT_LIB: load another build of the library (same-box A/B of two builds, tools/ab_env.sh)
+LIB_PATH = Path(os.environ.get("CLIPVIT_LIB") or Path(__file__).resolve().parent / "libclipvit_hip.so")
 
 F32, BF16, F16, MXFP8 = 0, 1, 2, 3
 OK, E_INVALID, E_HIP, E_STATE, E_NOMEM = 0, -1, -2, -3, -4

@@ -314,7 +314,7 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
 
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0>
-__global__ __launch_bounds__(64 * WM* WN) void gemm_pipe_kernel(GemmArgs a) {
+__global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM, TN = BN / WN;

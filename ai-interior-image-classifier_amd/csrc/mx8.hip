@@ -137,7 +137,7 @@ void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, u
 // ---------------------------------------------------------------------------------------
 // C[M, N] = dequant(A8)[M, K] @ dequant(W8)[N, K]^T (+ bias), fused epilogue.
 template <typename TO, int BM, int BN, int WM, int WN, int EPI>
-__global__ __launch_bounds__(64 * WM* WN) void gemm_mx8_kernel(GemmArgs a) {
+__global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
     constexpr int NT = 64 * WM * WN;
     constexpr int TM = BM / WM, TN = BN / WN;
     constexpr int FM = TM / 16, FN = TN / 16;
