@@ -149,8 +149,11 @@ struct clipvit_handle {
     // one-round tiles 92 / 93 win standalone (c_proj 67.4 -> 62.7 us, patch 75.2 -> 69.6) but
     // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158).
     // 98 = 240x256 QKV tiles of 12 waves (486 tiles = 1.9 rounds at bs 256 against 450 = 1.76
-    // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward
-    int var[5] = {98, 82, 13, 82, 22};
+    // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward. c_fc on 22 in one launch since
+    // the 4-wave tiles keep their accumulators in VGPRs (gemm_pipe_kernel launch bounds): c_fc
+    // 0.795 ms per forward as with the round split (8 + 81), c_proj after it 0.675 -> 0.658 ms,
+    // B/32 bs 256 85.6k -> 86.3k img/s (2 same-box alternations)
+    int var[5] = {98, 82, 22, 82, 22};
     bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
@@ -187,8 +190,9 @@ struct clipvit_handle {
     unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
     int max_inflight = 2;  // workspaces kept for calls in flight on different streams (CLIPVIT_MAX_INFLIGHT)
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
-    // whole-round row split of the 16-bit-output GEMMs (see gemm()); CLIPVIT_GEMM_SPLIT=0 disables
-    bool round_split = true;
+    // whole-round row split of the 16-bit-output GEMMs (see gemm()); off by default since c_fc
+    // runs on the 160x128 tile (var above); CLIPVIT_GEMM_SPLIT=1 enables
+    bool round_split = false;
     int split_main = 8, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
     // XCD map of the main launch (tile_of_block; CLIPVIT_SPLIT_XCD): 34 = the 1-D remap over a
     // column-group-major order with 2 N-groups, so each XCD group keeps half of W (2.4 MB of
