@@ -22,8 +22,11 @@ LIB = PKG_DIR / "libclipvit_hip.so"
 ARCH = "gfx950"
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# --amdgpu-mfma-vgpr-form: MFMA accumulators in VGPRs. Without it the backend put the
+# accumulators of tiles whose occupancy allows > 256 registers (the class-token tail's 2-wave
+# 64x64 tile) in AGPRs and rotated them with v_accvgpr_mov/read/write every k-step.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
-          "-Wno-unused-result", "-Wno-unused-value"]
+          "-mllvm", "--amdgpu-mfma-vgpr-form", "-Wno-unused-result", "-Wno-unused-value"]
 
 
 def _sources() -> list[Path]:
@@ -39,7 +42,7 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 
 def _compile(src: Path) -> tuple[Path, str]:
     obj = BUILD / (src.stem + ".o")
-    deps = [src, CSRC / "common.h", INCLUDE / "clipvit.h"]
+    deps = [src, CSRC / "common.h", INCLUDE / "clipvit.h", Path(__file__)]  # this file: the flags
     if not _needs(obj, deps):
         return obj, ""
     cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
