@@ -382,28 +382,49 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     // Staging by buffer loads over the tile's own rows (resource base = first row of the tile):
     // the 32-bit per-lane offsets stay constant over k and the k offset is an SGPR, so a k-step
     // issues no address arithmetic (global_load_lds needed a 64-bit add per piece; measured
-    // B/32 bs 256 83.3k -> 83.9k img/s, c_proj 0.739 -> 0.723 ms per forward). The implicit-GEMM
-    // patch path keeps per-lane global addresses (its k offset is not separable).
-    constexpr bool BUFL = PIMPL == 0;
+    // B/32 bs 256 83.3k -> 83.9k img/s, c_proj 0.739 -> 0.723 ms per forward).
+    // Implicit-GEMM patches with P | 64 and 64 | P^2 (P = 16, 32): a 64-deep k-tile is 64 / P
+    // whole pixel rows of one channel, so a piece's pixel offset = a per-lane part (row inside
+    // the k-tile, 8-pixel chunk) + a wave-uniform part of kt (channel, first row): the same
+    // buffer-load form, resource based at the tile's first image. P = 14 keeps per-lane
+    // patch_koff addresses (its channels are 224 k long: k-tiles straddle channels).
+    constexpr bool PSEP = PIMPL > 0 && 64 % PIMPL == 0 && (PIMPL * PIMPL) % 64 == 0;
+    constexpr bool BUFL = PIMPL == 0 || PSEP;
     i32x4_t rsA{}, rsW{};
     unsigned boa[BUFL ? LA : 1], bow[BUFL ? LW : 1];
     if constexpr (BUFL) {
-        const size_t abytes = (size_t)(a.M - m0) * ldb, wbytes = (size_t)(a.N - n0) * ldb;
-        rsA = buf_rsrc(Ab + (size_t)m0 * ldb, (unsigned)min(abytes, (size_t)0xFFFFFFFFu));
+        const size_t wbytes = (size_t)(a.N - n0) * ldb;
         rsW = buf_rsrc(Wb + (size_t)n0 * ldb, (unsigned)min(wbytes, (size_t)0xFFFFFFFFu));
 #pragma unroll
-        for (int r = 0; r < LA; ++r) boa[r] = (unsigned)(asrc[r] - (size_t)m0 * ldb);
-#pragma unroll
         for (int r = 0; r < LW; ++r) bow[r] = (unsigned)(wsrc[r] - (size_t)n0 * ldb);
+        if constexpr (PSEP) {
+            constexpr int CPR = PIMPL / 8;  // 16-B chunks per pixel row of a patch
+            const size_t img = (size_t)3 * a.patch_R * a.patch_Rw * 2;  // bytes per image
+            const int b0 = min(m0, mlast) / a.patch_g2, nimg = a.M / a.patch_g2;
+            rsA = buf_rsrc(Ab + b0 * img, (unsigned)min((size_t)(nimg - b0) * img, (size_t)0xFFFFFFFFu));
+#pragma unroll
+            for (int r = 0; r < LA; ++r)
+                boa[r] = (unsigned)(asrc[r] - b0 * img + 2 * ((acol[r] / CPR) * a.patch_Rw + 8 * (acol[r] % CPR)));
+        } else {
+            const size_t abytes = (size_t)(a.M - m0) * ldb;
+            rsA = buf_rsrc(Ab + (size_t)m0 * ldb, (unsigned)min(abytes, (size_t)0xFFFFFFFFu));
+#pragma unroll
+            for (int r = 0; r < LA; ++r) boa[r] = (unsigned)(asrc[r] - (size_t)m0 * ldb);
+        }
     }
     auto stage = [&](int buf, int kt) {
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = kbase + (size_t)kt * 128;
         if constexpr (BUFL) {
+            int aofs = (int)kofs;
+            if constexpr (PSEP) {  // channel kt / KPC, first pixel row (kt % KPC) * (64 / P)
+                constexpr int KPC = PIMPL * PIMPL / 64;
+                aofs = ((kt / KPC) * a.patch_R + (kt % KPC) * (64 / PIMPL)) * a.patch_Rw * 2;
+            }
 #pragma unroll
             for (int r = 0; r < LA; ++r)
-                if (r * NT * 16 + wave * 1024 < A_BYTES) blds16(rsA, boa[r], (int)kofs, sA + r * NT * 16 + wave * 1024);
+                if (r * NT * 16 + wave * 1024 < A_BYTES) blds16(rsA, boa[r], aofs, sA + r * NT * 16 + wave * 1024);
 #pragma unroll
             for (int r = 0; r < LW; ++r)
                 if (r * NT * 16 + wave * 1024 < W_BYTES) blds16(rsW, bow[r], (int)kofs, sW + r * NT * 16 + wave * 1024);
@@ -411,13 +432,9 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         }
 #pragma unroll
         for (int r = 0; r < LA; ++r)
-            if (r * NT * 16 + wave * 1024 < A_BYTES) {  // wave-uniform
-                if constexpr (PIMPL > 0)
-                    glds16(Ab + asrc[r] + 2 * (size_t)patch_koff<PIMPL>(kt * 64 + 8 * acol[r], a.patch_R, a.patch_Rw),
-                           sA + r * NT * 16 + wave * 1024);
-                else
-                    glds16(Ab + asrc[r] + kofs, sA + r * NT * 16 + wave * 1024);
-            }
+            if (r * NT * 16 + wave * 1024 < A_BYTES)  // wave-uniform
+                glds16(Ab + asrc[r] + 2 * (size_t)patch_koff<PIMPL>(kt * 64 + 8 * acol[r], a.patch_R, a.patch_Rw),
+                       sA + r * NT * 16 + wave * 1024);
 #pragma unroll
         for (int r = 0; r < LW; ++r)
             if (r * NT * 16 + wave * 1024 < W_BYTES)
