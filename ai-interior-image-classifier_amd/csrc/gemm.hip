@@ -416,6 +416,9 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = kbase + (size_t)kt * 128;
+#if CLIPVIT_ABLATE == 1  // diagnostic build only (tools/ablate.sh): no operand fill
+        return;
+#endif
         if constexpr (BUFL) {
             int aofs = (int)kofs;
             if constexpr (PSEP) {  // channel kt / KPC, first pixel row (kt % KPC) * (64 / P)
@@ -520,6 +523,9 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     };
     static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
     auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
+#if CLIPVIT_ABLATE == 2  // diagnostic build only (tools/ablate.sh): no MFMAs (fragment reads are dead too)
+        return;
+#endif
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
