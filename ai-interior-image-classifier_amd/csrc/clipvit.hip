@@ -511,6 +511,8 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
 
 // MX-fp8 encoder forward (same sequence as forward()). Blocks listed in
 // mx8_skip run the 16-bit path; every LayerNorm writes the format its consumer block uses.
+// resid16 (default): out_proj / c_proj store their bf16 branch outputs y, y2 in the dead qkv
+// buffer and the deferred add + LayerNorm kernels do the fp32 residual adds, as in forward().
 static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B,
                        Lane* w, float* f_out, Prof* prof) {
     const int D = h->D, N = h->N, M = B * N;
@@ -522,6 +524,13 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         if (q) launch_layernorm_q8(s, w->x, q8, q8s, g, b, M, D);
         else launch_layernorm(s, h->dt, w->x, w->h, g, b, M, D);
     };
+    // x (+)= y (+ y2), then LayerNorm into the next GEMM's operand format. yb = y2: x = (x + y) + y2
+    // stored; yb null: x + y, stored unless defer
+    auto add_ln = [&](const void* ya, const void* yb, const float* g, const float* b, bool q, bool defer) {
+        if (q) launch_add_layernorm_q8(s, w->x, ya, yb, q8, q8s, g, b, M, D, defer);
+        else if (yb || defer) launch_add_layernorm_deferred(s, h->dt, w->x, ya, yb, w->h, g, b, M, D);
+        else launch_add_layernorm(s, h->dt, w->x, ya, w->h, g, b, M, D);
+    };
     if (prof) prof->mark(s, F_EMBED);
     if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
@@ -532,9 +541,11 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
                         l0.ln1b, B, N, D);
     if (prof) prof->mark(s, F_EMBED);
+    void* y = w->qkv;
+    void* y2 = (u16*)w->qkv + (size_t)M * D;
     for (int i = 0; i < h->cfg.layers; ++i) {
         const LayerW& ly = h->layers[i];
-        const bool q = h->q8_layer(i);
+        const bool q = h->q8_layer(i), last = i + 1 == h->cfg.layers;
         rc = q ? gemm8(s, h, EPI_STORE, q8, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)
                : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV);
         if (rc) return rc;
@@ -542,27 +553,36 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
         if (prof) prof->mark(s, F_ATTN);
-        if (i + 1 == h->cfg.layers && h->cls_prune && !q) {  // bf16 last block: class-token rows only
+        if (last && h->cls_prune && !q) {  // bf16 last block: class-token rows only
             if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
         }
-        rc = q ? gemm8(s, h, EPI_RESID, q8, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT)
-               : gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT);
+        const bool r16 = h->resid16, defer = r16 && h->defer_x && !last;
+        const int eo = r16 ? EPI_STORE : EPI_RESID;
+        void* co = r16 ? y : (void*)w->x;
+        rc = q ? gemm8(s, h, eo, q8, ly.wout, ly.bout, co, M, D, D, D, R_OUT)
+               : gemm(s, h, eo, w->h, ly.wout, ly.bout, co, M, D, D, D, R_OUT);
         if (rc) return rc;
         if (prof) prof->mark(s, F_OUT);
-        ln(ly.ln2g, ly.ln2b, q);
+        if (r16) add_ln(y, nullptr, ly.ln2g, ly.ln2b, q, defer);
+        else ln(ly.ln2g, ly.ln2b, q);
         if (prof) prof->mark(s, F_LN);
         rc = q ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
                : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC);
         if (rc) return rc;
         if (prof) prof->mark(s, F_FC);
-        rc = q ? gemm8(s, h, EPI_RESID, u8, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ)
-               : gemm(s, h, EPI_RESID, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ);
+        const bool p16 = r16 && !last;
+        const int ep = p16 ? EPI_STORE : EPI_RESID;
+        void* cp = p16 ? (defer ? y2 : y) : (void*)w->x;
+        rc = q ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ)
+               : gemm(s, h, ep, w->u, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ);
         if (rc) return rc;
         if (prof) prof->mark(s, F_PROJ);
-        if (i + 1 < h->cfg.layers) {
-            ln(h->layers[i + 1].ln1g, h->layers[i + 1].ln1b, h->q8_layer(i + 1));
+        if (!last) {
+            const LayerW& nx = h->layers[i + 1];
+            if (p16) add_ln(y, defer ? y2 : nullptr, nx.ln1g, nx.ln1b, h->q8_layer(i + 1), false);
+            else ln(nx.ln1g, nx.ln1b, h->q8_layer(i + 1));
             if (prof) prof->mark(s, F_LN);
         }
     }
@@ -862,8 +882,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     h->dt = h->mx8 ? CLIPVIT_BF16 : c.compute_dtype;  // 16-bit type of everything not MX-fp8
     // 16-bit residual branch outputs for both 16-bit types (bf16 too since r02: measured 76.3k ->
     // 78.9k img/s at bs 256 with the logit error unchanged, 4.35e-3 -> 4.13e-3)
-    h->resid16 = !h->mx8;
-    if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = !h->mx8 && atoi(v) != 0;
+    h->resid16 = true;  // fp16, bf16 and MX-fp8 (its bf16 branch outputs)
+    if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
     // off by default: measured slower (the residual epilogues run in lockstep
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)

@@ -310,6 +310,9 @@ void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const voi
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D);
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
                          const float* g, const float* b, int rows, int D);
+// x (+)= y (+ y2), LayerNorm -> MX-fp8 q + scales sq (bf16 branch outputs of the MX-fp8 forward)
+void launch_add_layernorm_q8(hipStream_t s, float* x, const void* y, const void* y2, unsigned char* q,
+                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer);
 void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,
                         const float* cls, const float* pos, const float* g_pre,
                         const float* b_pre, const float* g1, const float* b1, int B, int N, int D);

@@ -272,10 +272,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // x[row] += y[row] (16-bit branch output of out_proj / c_proj); h[row] = LayerNorm(x[row]).
 // Moves the residual add out of the GEMM epilogue (which then only stores y): the GEMM no
 // longer reads x, and this kernel streams x, y -> x, h in one pass.
-template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1>
+// Q8: h is the MX-fp8 A operand of the next GEMM (q [rows][D] + E8M0 scales sq [rows][D/32]).
+template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
-                                                            u16* __restrict__ h, const float* __restrict__ gm,
+                                                            void* __restrict__ h, unsigned char* __restrict__ sq,
+                                                            const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
     // RPW rows per wave, every row's loads issued before any row's arithmetic (more bytes in
     // flight per wave; rows / RPW waves fit one residency round of the CUs at bs 256)
@@ -318,7 +320,8 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
             if constexpr (STORE_X) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
         }
         ln_row<V>(v[r], gm, bt, lane, (float)D);
-        store_row16<T, V>(h + (size_t)row * D, v[r], lane);
+        if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v[r], lane);
+        else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
     }
 }
 
@@ -443,9 +446,9 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
                           const float* b, int rows, int D) {
     dim3 grid((rows + 3) / 4), block(256);
     if (dtype == 2) {
-        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
+        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, h, nullptr, g, b, rows));
     } else {
-        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, (u16*)h, g, b, rows));
+        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, h, nullptr, g, b, rows));
     }
 }
 
@@ -453,8 +456,23 @@ template <typename T, int V>
 static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
     dim3 grid((rows + 3) / 4), block(256);
-    if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, g, b, rows);
-    else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, g, b, rows);
+    if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+    else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+}
+
+// MX-fp8 forms (bf16 branch outputs): y2 given -> x = (x + y) + y2 stored; y2 null -> x + y not
+// stored when defer (the add after out_proj), stored otherwise; LayerNorm -> q8 + scales
+template <int V>
+static void add_ln_q8(hipStream_t s, float* x, const u16* y, const u16* y2, unsigned char* q, unsigned char* sq,
+                      const float* g, const float* b, int rows, bool defer) {
+    dim3 grid((rows + 3) / 4), block(256);
+    if (y2) add_layernorm_kernel<BF16, V, true, true, 1, true><<<grid, block, 0, s>>>(x, y, y2, q, sq, g, b, rows);
+    else if (defer) add_layernorm_kernel<BF16, V, false, false, 1, true><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
+    else add_layernorm_kernel<BF16, V, true, false, 1, true><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
+}
+void launch_add_layernorm_q8(hipStream_t s, float* x, const void* y, const void* y2, unsigned char* q,
+                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer) {
+    DISPATCH_V(D, add_ln_q8<V>(s, x, (const u16*)y, (const u16*)y2, q, sq, g, b, rows, defer));
 }
 
 void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, int S, const float* bias,
