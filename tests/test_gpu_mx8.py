@@ -198,24 +198,28 @@ def test_mxfp8_logits_within_config5_bar(gpu):
         e8.close()
 
 
-@pytest.mark.parametrize("skip,resid16", [("", "1"), ("0,1,10,11", "0")])
-def test_mxfp8_forward_variants(gpu, monkeypatch, skip, resid16):
+@pytest.mark.parametrize("model,skip,resid16", [("ViT-B/32", "", "1"), ("ViT-B/32", "0,1,10,11", "0"),
+                                               ("ViT-B/16", None, None)])
+def test_mxfp8_forward_variants(gpu, monkeypatch, model, skip, resid16):
     """The MX-fp8 forward's other block layouts: every block MX-fp8 (CLIPVIT_MX8_SKIP="": the last
-    block runs on all rows, its c_proj adds into x in the MX GEMM epilogue, no class-token tail)
-    and the fp32 read-modify-write residual adds (CLIPVIT_RESID16=0, the pre-r02 path). Against
-    the bf16 engine at CLIP logit scale: embeddings aligned and logits within the all-MX-fp8
-    figure of DESIGN.md 5.7 (2.0e-2) plus margin."""
-    cfg = C.get_config("ViT-B/32")
+    block runs on all rows, its c_proj adds into x in the MX GEMM epilogue, no class-token tail),
+    the fp32 read-modify-write residual adds (CLIPVIT_RESID16=0, the pre-r02 path), and the
+    default layout on ViT-B/16 (N = 197). Against the bf16 engine at CLIP logit scale:
+    embeddings aligned and logits within the all-MX-fp8 figure of DESIGN.md 5.7 (2.0e-2) plus
+    margin."""
+    cfg = C.get_config(model)
     sd = synthetic_state_dict(cfg, 0)
     adapters = synthetic_adapters(cfg, rank=8)
     g = torch.Generator().manual_seed(77)
     segs = [0, 40, 60, 359, 395, 425, 437]
     B = 16
-    px = torch.randn(B, 3, 224, 224, generator=g).clamp_(-1.8, 2.2).to(gpu)
+    px = torch.randn(B, 3, cfg.image_size, cfg.image_size, generator=g).clamp_(-1.8, 2.2).to(gpu)
     T0 = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
     e16 = _engine(cfg, "bf16", sd, adapters, T0, segs, gpu, B)
-    monkeypatch.setenv("CLIPVIT_MX8_SKIP", skip)
-    monkeypatch.setenv("CLIPVIT_RESID16", resid16)
+    if skip is not None:
+        monkeypatch.setenv("CLIPVIT_MX8_SKIP", skip)
+    if resid16 is not None:
+        monkeypatch.setenv("CLIPVIT_RESID16", resid16)
     e8 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B)
     try:
         f16 = e16.encode_image(px).cpu()
@@ -227,7 +231,7 @@ def test_mxfp8_forward_variants(gpu, monkeypatch, skip, resid16):
         l16, l8 = r16.logits.cpu(), r8.logits.cpu()
         rel = ((l8 - l16).abs().amax(1) / l16.abs().amax(1)).max().item()
         cos = torch.nn.functional.cosine_similarity(r8.emb.cpu(), r16.emb.cpu(), dim=-1).min().item()
-        print(f"mxfp8 [skip '{skip}', resid16 {resid16}] vs bf16: max rel logit err {rel:.4g}, min emb cosine {cos:.6f}")
+        print(f"mxfp8 {model} [skip {skip!r}, resid16 {resid16}] vs bf16: max rel logit err {rel:.4g}, min emb cosine {cos:.6f}")
         assert cos > 0.99 and rel <= 3e-2, (rel, cos)
     finally:
         e16.close()
