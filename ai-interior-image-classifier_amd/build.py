@@ -27,6 +27,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # 64x64 tile) in AGPRs and rotated them with v_accvgpr_mov/read/write every k-step.
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-mllvm", "--amdgpu-mfma-vgpr-form", "-Wno-unused-result", "-Wno-unused-value"]
+# Per-source flags. gemm.hip: the max-memory-clause machine scheduler (clusters each k-step's
+# staging loads). Same-box A/B of the two builds: B/32 +0.2 / +0.6 %, B/16
+# +0.5 %, L/14@336 +0.7 / +1.0 % img/s, patch GEMM -7 %; on attention.hip it cost 6 %, so
+# only the GEMMs get it.
+SRC_FLAGS = {"gemm": ["-mllvm", "--amdgpu-sched-strategy=max-memory-clause"]}
 
 
 def _sources() -> list[Path]:
@@ -45,7 +50,7 @@ def _compile(src: Path) -> tuple[Path, str]:
     deps = [src, CSRC / "common.h", INCLUDE / "clipvit.h", Path(__file__)]  # this file: the flags
     if not _needs(obj, deps):
         return obj, ""
-    cmd = [HIPCC, *CFLAGS, "-c", str(src), "-o", str(obj)]
+    cmd = [HIPCC, *CFLAGS, *SRC_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
