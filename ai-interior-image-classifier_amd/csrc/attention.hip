@@ -176,7 +176,8 @@ __global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ 
 // lane i receives column d = 16 dt + i of the 4 keys — the A operand of O^T += V^T P^T with
 // the k order of P (k-slot (g, e) <-> key 32 st + 16 (e >> 2) + 4 g + (e & 3)). No scalar
 // LDS transposes, no __syncthreads (raw s_barrier + counted vmcnt keep the next block's loads
-// in flight). Rows past the sequence are clamped in bounds and masked to -inf in S.
+// in flight). Key rows past the sequence read as zeros (outside the rebased buffer range) and
+// are masked to -inf in S.
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // QW waves per workgroup = 16 QW queries; every wave loads 64 / QW key rows of K and of V
@@ -210,20 +211,24 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
     // glds assignment: wave w fills key rows [RW w, RW w + RW) of K and of V (1 KB pieces)
     constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
     // K/V staging by buffer loads over this image's rows: per-lane offsets constant over the key
-    // blocks, the block's offset in an SGPR; key rows >= N lie past the resource's range and read
-    // as zeros (their scores are masked, and P = 0 there)
+    // blocks. The resource is rebased at every key block (base += block offset, range -= block
+    // offset: scalar arithmetic), because the hardware range check covers the per-lane offset
+    // only, not an SGPR offset. Key rows >= N then lie past the range in every block and read
+    // as zeros (their scores are masked, and P = 0 there); nothing past this image's last key row
+    // is ever fetched (tests/test_gpu_kernels.py::test_attention_tail_rows_never_read).
     const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
-    const i32x4_t rs = buf_rsrc(src, (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128));
+    const unsigned range = (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128);
     auto issue = [&](int kb, int st) {
         unsigned char* dst = smem + st * STAGE;
-        const int kofs = kb * 64 * ld * 2;
+        const unsigned kofs = (unsigned)(kb * 64 * ld * 2);
+        const i32x4_t rs = buf_rsrc(src + kofs, range - kofs);
 #pragma unroll
         for (int r = 0; r < RW / 8; ++r) {
             const int row = wave * RW + r * 8 + (lane >> 3);
             const int c = (lane & 7) ^ (row & 7);
             const unsigned off = (unsigned)(row * ld * 2 + c * 16);
-            blds16(rs, off, kofs, dst + (wave * RW + r * 8) * 128);
-            blds16(rs, off + (unsigned)D * 2, kofs, dst + 8192 + (wave * RW + r * 8) * 128);
+            blds16(rs, off, 0, dst + (wave * RW + r * 8) * 128);
+            blds16(rs, off + (unsigned)D * 2, 0, dst + 8192 + (wave * RW + r * 8) * 128);
         }
     };
 
@@ -412,20 +417,24 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
 
     constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // rows per wave, glds per thread per block
     // K/V staging by buffer loads over this image's rows: per-lane offsets constant over the key
-    // blocks, the block's offset in an SGPR; key rows >= N lie past the resource's range and read
-    // as zeros (their scores are masked, and P = 0 there)
+    // blocks. The resource is rebased at every key block (base += block offset, range -= block
+    // offset: scalar arithmetic), because the hardware range check covers the per-lane offset
+    // only, not an SGPR offset. Key rows >= N then lie past the range in every block and read
+    // as zeros (their scores are masked, and P = 0 there); nothing past this image's last key row
+    // is ever fetched (tests/test_gpu_kernels.py::test_attention_tail_rows_never_read).
     const unsigned char* src = (const unsigned char*)(qkv + base * ld + D + h * 64);
-    const i32x4_t rs = buf_rsrc(src, (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128));
+    const unsigned range = (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128);
     auto issue = [&](int kb, int st) {
         unsigned char* dst = smem + st * STAGE;
-        const int kofs = kb * 64 * ld * 2;
+        const unsigned kofs = (unsigned)(kb * 64 * ld * 2);
+        const i32x4_t rs = buf_rsrc(src + kofs, range - kofs);
 #pragma unroll
         for (int r = 0; r < RW / 8; ++r) {
             const int row = wave * RW + r * 8 + (lane >> 3);
             const int c = (lane & 7) ^ (row & 7);
             const unsigned off = (unsigned)(row * ld * 2 + c * 16);
-            blds16(rs, off, kofs, dst + (wave * RW + r * 8) * 128);
-            blds16(rs, off + (unsigned)D * 2, kofs, dst + 8192 + (wave * RW + r * 8) * 128);
+            blds16(rs, off, 0, dst + (wave * RW + r * 8) * 128);
+            blds16(rs, off + (unsigned)D * 2, 0, dst + 8192 + (wave * RW + r * 8) * 128);
         }
     };
 

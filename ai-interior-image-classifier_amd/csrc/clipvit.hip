@@ -1220,11 +1220,27 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
             acc[p.fam[k]] += ms;
         }
     }
+    // intervals per family in one forward (an event closes every interval), and the device
+    // time between two back-to-back events with no work between them: the per-interval cost of
+    // the marks themselves, which the family times above include
+    int cnt[F_COUNT] = {0};
+    for (size_t k = 1; k < p.k; ++k) ++cnt[p.fam[k]];
+    float gap = 0.f;
+    if (!rc) {
+        constexpr int NG = 17;
+        for (int k = 0; k < NG; ++k) hipEventRecord(p.ev[k], s);
+        hipEventSynchronize(p.ev[NG - 1]);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, p.ev[0], p.ev[NG - 1]);
+        gap = ms / (NG - 1);
+    }
     hipEventRecord(l->done, s);
     for (auto& e : p.ev) hipEventDestroy(e);
     release_ws(h, w);
     for (int f = 0; f < F_COUNT; ++f) out_ms[f] = (float)(acc[f] / iters);
     out_ms[F_COUNT] = (float)Bl;
+    for (int f = 0; f < F_COUNT; ++f) out_ms[F_COUNT + 1 + f] = (float)cnt[f];
+    out_ms[2 * F_COUNT + 1] = gap;
     return rc;
 }
 

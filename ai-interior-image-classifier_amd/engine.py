@@ -175,13 +175,17 @@ class VisionEngine:
     def profile_forward(self, pixels: torch.Tensor, iters: int = 5) -> dict[str, float]:
         """Per-kernel-family device milliseconds of one forward (HIP events between stages)."""
         pixels = self._pixels(pixels)
-        ms = (ctypes.c_float * 10)()
+        ms = (ctypes.c_float * 20)()
         with torch.cuda.device(self.device):
             _lib.check(self._L.clipvit_profile_forward(self._h, self._stream(), _vp(pixels),
                                                        _PIX_DT[pixels.dtype], pixels.shape[0], iters, ms))
-        keys = ("patch_embed", "qkv_gemm", "attention", "out_proj_gemm", "layernorm", "fc_gemm",
-                "proj_gemm", "head", "cls_tail", "lane_batch")
-        return {k: float(v) for k, v in zip(keys, ms)}
+        fams = ("patch_embed", "qkv_gemm", "attention", "out_proj_gemm", "layernorm", "fc_gemm",
+                "proj_gemm", "head", "cls_tail")
+        out = {k: float(v) for k, v in zip(fams, ms)}
+        out["lane_batch"] = float(ms[9])
+        out["intervals"] = {k: int(ms[10 + i]) for i, k in enumerate(fams)}
+        out["event_gap_ms"] = float(ms[19])
+        return out
 
 
 # ------------------------------------------------------------------ kernel-level helpers

@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define CLIPVIT_ABI_VERSION 1
+/* 2: clipvit_attention_test takes `causal` (8 arguments; version 1 had 7). */
+#define CLIPVIT_ABI_VERSION 2
 
 /* Status codes. */
 #define CLIPVIT_OK 0
@@ -251,11 +252,17 @@ int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* o
 
 /* Time `iters` launches of ONE lane's encoder forward (the per-stream batch the call path
  * launches for B images: ceil(B/2) when the batch is split over the two lane streams, else B)
- * serialised on `stream`; returns the average per-kernel-family device time (ms) into
- * out_ms[0..8]: 0 patch+embed, 1 qkv gemm, 2 attention, 3 out-proj gemm, 4 layernorm,
- * 5 fc gemm, 6 proj gemm, 7 head (ln_post+proj), 8 the last block's row-wise part on
- * class-token rows (0 when the full last block runs); out_ms[9] = the lane batch profiled.
- * Requires weights loaded. Used by bench.py's roofline probe. */
+ * serialised on `stream`, with a HIP event closing every kernel-family interval; out_ms must
+ * hold 20 floats:
+ *   out_ms[0..8]   average device time (ms) per family and forward: 0 patch+embed, 1 qkv gemm,
+ *                  2 attention, 3 out-proj gemm, 4 layernorm, 5 fc gemm, 6 proj gemm, 7 head
+ *                  (ln_post+proj), 8 the last block's row-wise part on class-token rows (0 when
+ *                  the full last block runs);
+ *   out_ms[9]      the lane batch profiled;
+ *   out_ms[10..18] event intervals per family and forward (same order as 0..8);
+ *   out_ms[19]     device time (ms) between two back-to-back events with no work between them
+ *                  (the per-interval cost of the marks, included in out_ms[0..8]).
+ * Requires weights loaded. Used by bench.py's roofline probe. (ABI version 2.) */
 int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype,
                             int B, int iters, float* out_ms);
 

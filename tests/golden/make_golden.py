@@ -18,8 +18,13 @@ list learned from the reference's own prompt vocabulary; everything AFTER ``clip
     -> harness_<model>_<ckpt>.json (result dicts of analyze_images_batch with and without the
     interior filter, is_interior_image per image, label order) + harness_<model>_<ckpt>.npz
     (the harness's 100*cos logits [151, 40 + C], its L2-normalised image features and pixel
-    checksums) + text_<ckpt>.npz (the
-    detector's and the analyzer's cached text matrices).
+    checksums) + text_<ckpt>.npz (the detector's and the analyzer's cached text matrices), and
+    the single-image surface: analyze_image_from_url on the first 16 images, filter on / off.
+  * The same harness calls at CLIP's logit scale: after the analyzer is
+    built, ``an.text_features_cache`` and ``an.detector.text_features`` are overwritten with
+    rows normalise(0.3 f + 0.95 r) (f = the reference's fp32 image features, r seeded random
+    unit vectors: max|logit| ~ 30); everything downstream is main.py's code
+    -> harness_<model>_<ckpt>_clipscale.{json,npz} + clipscale_text_<model>.npz.
   * Copies the input JPEGs, interior_dataset.json and the two LoRA checkpoints (data files the
     reference reads at run time) into tests/golden/ so the GPU-box tests need nothing from
     /root/reference; writes the learned merges to bpe_merges.txt.
@@ -111,7 +116,48 @@ def lora_facts(torch, ref_main, shim, ckpt_name):
     }
 
 
-def harness(torch, ref_main, shim, model_name, ckpt):
+SINGLE = IMAGES[:16]     # the single-image surface (analyze_image_from_url, bs 1)
+CLIP_SCALE_SEED = 42
+
+
+def _run_harness(torch, ref_main, an, paths):
+    """The reference's own calls on one analyzer: analyze_images_batch (filter on / off),
+    is_interior_image per image, analyze_image_from_url on SINGLE (filter on / off; the URL
+    loader is stubbed by a local-file open, the one network call in the path)."""
+    from PIL import Image
+    with torch.no_grad():
+        res_f = an.analyze_images_batch(paths, batch_size=16, filter_interiors=True,
+                                        confidence_threshold=0.3)
+        res_nf = an.analyze_images_batch(paths, batch_size=16, filter_interiors=False)
+        det = [list(an.detector.is_interior_image(Image.open(p).convert("RGB"), 0.3)) for p in paths]
+        loader = ref_main.URLImageLoader.load_image_from_url
+        ref_main.URLImageLoader.load_image_from_url = staticmethod(lambda url, timeout=30: Image.open(url).convert("RGB"))
+        try:
+            single = {flt: {Path(p).name: an.analyze_image_from_url(str(REF / p), filter_interiors=flt) for p in SINGLE}
+                      for flt in (True, False)}
+        finally:
+            ref_main.URLImageLoader.load_image_from_url = loader
+    key = lambda p: Path(p).name
+    return {"detector": {key(p): d for p, d in zip(IMAGES, det)},
+            "filter_true": {key(k): v for k, v in res_f.items()},
+            "filter_false": {key(k): v for k, v in res_nf.items()},
+            "single_filter_true": single[True], "single_filter_false": single[False]}
+
+
+def clip_scale_text(torch, f, sizes):
+    """CLIP-scale label rows: row c = normalise(0.3 f[c mod n] +
+    0.95 r_c) with f = the reference's fp32 L2-normalised features of the fixture images and r_c
+    seeded random unit vectors, so every image's best labels sit at 100 cos ~ 30 like real CLIP.
+    Returns one matrix per segment (sizes = rows per segment, detector first)."""
+    g = torch.Generator().manual_seed(CLIP_SCALE_SEED)
+    C = sum(sizes)
+    r = torch.nn.functional.normalize(torch.randn(C, f.shape[1], generator=g, dtype=torch.float64), dim=-1)
+    T = 0.3 * f.double()[torch.arange(C) % f.shape[0]] + 0.95 * r
+    T = (T / T.norm(dim=-1, keepdim=True)).float()
+    return list(torch.split(T, sizes))
+
+
+def harness(torch, ref_main, shim, model_name, ckpt, clip_scale=True):
     from PIL import Image
     base_load = shim.base_load  # every clip.load(...) of the harness gets `model_name` weights
     ref_main.clip.load = lambda name, device="cpu", **kw: base_load(model_name, device)
@@ -122,46 +168,54 @@ def harness(torch, ref_main, shim, model_name, ckpt):
                                              lora_rank=4, lora_alpha=8, device="cpu")
         paths = [str(REF / p) for p in IMAGES]
         with torch.no_grad():
-            res_f = an.analyze_images_batch(paths, batch_size=16, filter_interiors=True,
-                                            confidence_threshold=0.3)
-            res_nf = an.analyze_images_batch(paths, batch_size=16, filter_interiors=False)
-            det = [list(an.detector.is_interior_image(Image.open(p).convert("RGB"), 0.3)) for p in paths]
             pix = torch.stack([an.preprocess(Image.open(p).convert("RGB")) for p in paths])
             f = torch.cat([an.model.encode_image(pix[a:a + 16]) for a in range(0, len(paths), 16)])
             f = f / f.norm(dim=-1, keepdim=True)
+        runs = {}
+        for scale in ((False, True) if clip_scale else (False,)):
+            if scale:  # the harness's caches replaced by CLIP-scale rows; all else is main.py's code
+                segs = list(an.text_features_cache.keys())
+                mats = clip_scale_text(torch, f, [len(an.detector.categories)] +
+                                       [an.text_features_cache[c].shape[0] for c in segs])
+                an.detector.text_features = mats[0]
+                for c, m in zip(segs, mats[1:]):
+                    an.text_features_cache[c] = m
+            res = _run_harness(torch, ref_main, an, paths)
             T = {c: t.float().numpy() for c, t in an.text_features_cache.items()}
             T_det = an.detector.text_features.float().numpy()
             logits = 100.0 * f @ torch.cat([torch.from_numpy(T_det)] + [torch.from_numpy(T[c]) for c in T]).t()
+            runs[scale] = (res, T, T_det, logits)
     finally:
         os.chdir(cwd)
-    key = lambda p: Path(p).name
-    out = {
-        "model": model_name,
-        "checkpoint": ckpt,
-        "weights_seed": WEIGHT_SEED,
-        "text_seed": TEXT_SEED,
-        "pythonhashseed": os.environ.get("PYTHONHASHSEED"),
-        "images": [Path(p).name for p in IMAGES],
-        "categories": an.all_categories,
-        "segments": list(T.keys()),
-        "detector_categories": an.detector.categories,
-        "detector": {Path(p).name: d for p, d in zip(IMAGES, det)},
-        "filter_true": {key(k): v for k, v in res_f.items()},
-        "filter_false": {key(k): v for k, v in res_nf.items()},
-    }
-    flat = pix.reshape(len(IMAGES), -1)
-    idx = torch.arange(0, flat.shape[1], 151)  # 997 fixed sample positions per image
-    arrays = {"logits": logits.numpy(), "features": f.numpy(),
-              "pixels_sum": flat.double().sum(1).numpy(), "pixels_abs_sum": flat.double().abs().sum(1).numpy(),
-              "pixels_sample": flat[:, idx].numpy(), "pixels_sample_idx": idx.numpy()}
-    text = {"T_det": T_det, **{f"T_{c}": t for c, t in T.items()}}
-    return out, arrays, text
+    outs = {}
+    for scale, (res, T, T_det, logits) in runs.items():
+        out = {
+            "model": model_name,
+            "checkpoint": ckpt,
+            "weights_seed": WEIGHT_SEED,
+            "text_seed": TEXT_SEED,
+            "clip_scale_seed": CLIP_SCALE_SEED if scale else None,
+            "pythonhashseed": os.environ.get("PYTHONHASHSEED"),
+            "images": [Path(p).name for p in IMAGES],
+            "categories": an.all_categories,
+            "segments": list(T.keys()),
+            "detector_categories": an.detector.categories,
+            **res,
+        }
+        flat = pix.reshape(len(IMAGES), -1)
+        idx = torch.arange(0, flat.shape[1], 151)  # 997 fixed sample positions per image
+        arrays = {"logits": logits.numpy(), "features": f.numpy(),
+                  "pixels_sum": flat.double().sum(1).numpy(), "pixels_abs_sum": flat.double().abs().sum(1).numpy(),
+                  "pixels_sample": flat[:, idx].numpy(), "pixels_sample_idx": idx.numpy()}
+        text = {"T_det": T_det, **{f"T_{c}": t for c, t in T.items()}}
+        outs[scale] = (out, arrays, text)
+    return outs
 
 
 def main():
     if os.environ.get("PYTHONHASHSEED") != "0":
         env = dict(os.environ, PYTHONHASHSEED="0")
-        sys.exit(subprocess.call([sys.executable, __file__], env=env))
+        sys.exit(subprocess.call([sys.executable, __file__] + sys.argv[1:], env=env))
     import numpy as np
     torch, ref_main, shim, checks = _setup()
     (HERE / "images").mkdir(exist_ok=True)
@@ -174,12 +228,20 @@ def main():
     facts = {**checks, "checkpoints": [lora_facts(torch, ref_main, shim, c) for c in CKPTS]}
     (HERE / "lora_binding.json").write_text(json.dumps(facts, indent=1, ensure_ascii=False))
     for c in CKPTS:
+        ck = c.replace("comprehensive_", "").replace(".pth", "")
         for m in MODELS:
-            out, arrays, text = harness(torch, ref_main, shim, m, c)
+            outs = harness(torch, ref_main, shim, m, c)
             tag = tag_of(m, c)
-            (HERE / f"harness_{tag}.json").write_text(json.dumps(out, ensure_ascii=False))
-            np.savez_compressed(HERE / f"harness_{tag}.npz", **arrays)
-            np.savez_compressed(HERE / f"text_{c.replace('comprehensive_', '').replace('.pth', '')}.npz", **text)
+            for scale, (out, arrays, text) in outs.items():
+                sfx = "_clipscale" if scale else ""
+                (HERE / f"harness_{tag}{sfx}.json").write_text(json.dumps(out, ensure_ascii=False))
+                if scale:  # features and pixels are those of the flat run; the CLIP-scale rows per model
+                    np.savez_compressed(HERE / f"harness_{tag}{sfx}.npz", logits=arrays["logits"])
+                    mtag = tag_of(m, c).split("_")[0]
+                    np.savez_compressed(HERE / f"clipscale_text_{mtag}.npz", **text)
+                else:
+                    np.savez_compressed(HERE / f"harness_{tag}.npz", **arrays)
+                    np.savez_compressed(HERE / f"text_{ck}.npz", **text)
             print("wrote", tag, flush=True)
 
 

@@ -29,11 +29,12 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # variant = 100 * xcd_partition + tile kernel (gemm.hip launch_t); 2xx = 4x2 XCD tile partition,
 # 34xx / 35xx = column-group-major 1-D remap with 2 / 3 N-groups (tile_of_block).
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 13 / 81 128x128, 22 / 82 160x128,
-# 98 240x256 (12 waves), 90 64x64 (class-token tail); 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 13, 22, 80, 81, 82, 90, 98, 208, 213, 222, 280, 282, 298, 3408, 3513, 3480]
+# 98 240x256 (12 waves), 90 64x64 (class-token tail), 60 / 61 the 256x256 ping-pong tile (gemm_pp.hip,
+# direct / LDS-staged 16-bit stores); 2xx = the production XCD partition.
+VARIANTS = [1, 2, 3, 8, 13, 22, 60, 61, 80, 81, 82, 90, 98, 208, 213, 222, 260, 280, 282, 298, 3408, 3513, 3460, 3480]
 N128 = (1, 2, 13, 22, 81, 82)
-N256 = (3, 8, 80, 98)
-STAGED = (80, 81, 82, 98)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
+N256 = (3, 8, 60, 61, 80, 98)
+STAGED = (61, 80, 81, 82, 98)  # LDS-staged row-contiguous 16-bit epilogue (outputs rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -48,6 +49,8 @@ def _skip(variant, N, K):
     v = variant % 100
     if (v in N128 and N % 128) or (v in N256 and N % 256):
         return "tile does not divide N"
+    if v in (60, 61) and K % 128:
+        return "ping-pong tile: K in pairs of 64-deep k-tiles"
     return None
 
 
@@ -69,7 +72,7 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("variant", STAGED + (8, 13, 22))
+@pytest.mark.parametrize("variant", STAGED + (8, 13, 22, 60))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous
@@ -190,5 +193,22 @@ def test_attention_spiky_scores(gpu):
     qkv = qkv.to(torch.float16)
     out = E.attention_test(qkv, B, N, H)
     ref = _ref_attention(qkv, B, N, H)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 3e-3, err
+
+
+@pytest.mark.parametrize("B,N,H,causal", [(2, 77, 8, True), (2, 197, 12, False), (1, 577, 16, False),
+                                          (2, 130, 12, False), (1, 65, 12, False), (3, 50, 12, False)])
+def test_attention_tail_rows_never_read(gpu, B, N, H, causal):
+    """qkv is a view into a larger buffer whose rows after B*N are NaN. Key rows past N in the
+    last key block must never be fetched (a range check that misses an SGPR block
+    offset would read them), so the output stays finite and matches the reference."""
+    g = torch.Generator(device=gpu).manual_seed(B * N + H)
+    big = torch.full((B * N + 128, 3 * H * 64), float("nan"), device=gpu, dtype=torch.float16)
+    big[:B * N] = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).half()
+    qkv = big[:B * N]
+    out = E.attention_test(qkv, B, N, H, causal=causal)
+    assert torch.isfinite(out).all()
+    ref = _ref_attention(qkv, B, N, H, causal=causal)
     err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 3e-3, err
