@@ -155,6 +155,11 @@ struct clipvit_handle {
     // B/32 bs 256 85.6k -> 86.3k img/s (2 same-box alternations)
     int var[5] = {98, 82, 22, 82, 22};
     bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
+    // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
+    // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
+    // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
+    // 2,388 (same-box A/B). CLIPVIT_LARGE_VARIANTS="q,f"
+    int large_var[2] = {3462, 3462};
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -403,8 +408,14 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // (c_fc's QuickGELU epilogue stores directly from the accumulators, v8: measured L/14@336
     // c_fc 7.79 -> 7.52 ms, B/16 1.59 -> 1.52 ms per lane-forward against the LDS-staged v80)
     if (!h->var_forced && role != R_PATCH &&
-        (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu)))
+        (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu))) {
         variant = epi == EPI_GELU ? 8 : 80;
+        const int lv = role == R_QKV ? h->large_var[0] : role == R_FC ? h->large_var[1] : 0;
+        if (lv && (epi == EPI_STORE || epi == EPI_GELU)) {
+            a.xcd_n = lv / 100;
+            variant = lv % 100;
+        }
+    }
     // a tuned variant that does not tile this shape falls back to the shape-based choice
     if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -940,6 +951,10 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
             h->ncu = ncu;
     }
+    if (const char* v = getenv("CLIPVIT_LARGE_VARIANTS")) {
+        h->large_var[0] = atoi(v);
+        if (const char* c = strchr(v, ',')) h->large_var[1] = atoi(c + 1);
+    }
     if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
         h->var_forced = true;
         int k = 0;
@@ -1288,9 +1303,10 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
-    // LDS-staged 16-bit-output variants (80-82, 98), or epi 10 / 11 = 16-bit STORE / GELU on
+    // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
-    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98;
+    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 60 ||
+                        variant == 61 || variant == 62;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;
@@ -1382,6 +1398,7 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.patch_g2 = 49; a.patch_ntok = 50;
     a.xcd_n = variant / 100;
     variant %= 100;
+    if (const char* v = getenv("CLIPVIT_PP_DELAY")) a.pp_delay = atoi(v);  // bench of the stagger
     int e = epi;  // raw Epi enum
     if (mx) {
         a.sA = (const unsigned char*)A + (size_t)M * K;

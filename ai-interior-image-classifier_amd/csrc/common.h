@@ -169,6 +169,10 @@ struct GemmArgs {
     // split-K (EPI_F32 on the pipelined tiles only): grid.y = ksplit slices of K / ksplit each;
     // slice z writes its fp32 partial (no bias) to C + z * M * ldc. 0 / 1 = no split
     int ksplit;
+    // persistent ping-pong GEMM (gemm_pp.hip, variant 62): workgroups with fewer tiles than the
+    // busiest ones start pp_delay x 8k cycles x (their rank mod 4) / 4 late, so the epilogue store
+    // bursts of a round do not all fall at once (0 = off)
+    int pp_delay;
 };
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
@@ -277,6 +281,9 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
 // ---- launchers (defined in the .hip translation units) ----
 // variant: 0 = auto by shape; tile variants listed in gemm.hip launch_t
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
+// ping-pong 256x256 GEMM (gemm_pp.hip): variant 60 direct stores, 61 LDS-staged stores;
+// EPI_STORE / EPI_GELU, N % 256 == 0, K % 128 == 0
+int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
 // implicit-GEMM patch embedding (no im2col): P = patch size (14, 16, 32), a.A = pixels
 int launch_patch_gemm(hipStream_t s, int dtype, int P, const GemmArgs& a);
 // pixels of any supported dtype -> 16-bit pixels of the compute type (same [B, 3, R, R] layout)

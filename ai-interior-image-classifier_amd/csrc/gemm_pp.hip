@@ -1,0 +1,569 @@
+// Ping-pong MFMA GEMM: 256x256 tiles, 8 waves in two wave groups staggered by one barrier.
+//
+//   C[M, N] = A[M, K] @ W[N, K]^T + bias (16-bit C; QuickGELU for c_fc)
+//
+// Same operand conventions as gemm.hip (K-major A and packed W, swapped MFMA operands so a lane
+// owns one token and 16 contiguous features, LDS rows of 128 B with 16-B chunk c of row r at
+// c ^ (r & 7)), different schedule:
+//
+//  * waves 0-3 (group 0) and 4-7 (group 1) each own 128 token rows x 64 features per wave
+//    (wave w: rows 128 (w >> 2) .., features 64 (w & 3) ..); each SIMD hosts one wave of each
+//    group. Every 64-deep k-tile is four phases (one 64x32 quadrant of the wave's tile each,
+//    16 MFMAs): [LDS fragment reads + LDS-DMA issue] barrier [MFMAs] barrier. Group 1 runs one
+//    barrier behind group 0, so on every SIMD one wave's MFMAs cover the other wave's reads,
+//    DMA issue and barrier wait, and the matrix pipe is never idle at a barrier;
+//  * operand staging by buffer_load ... lds into two 64 KB stages; the loads of k-tile j are
+//    spread over the six phases in which their LDS rows are free (group 0 stages A, group 1
+//    stages W, two 1-KB pieces per wave per phase) and waited for by counted vmcnt — never 0
+//    in the loop — so they stay in flight across barriers;
+//  * schedule (slot = barrier interval; group g's phase P reads in slot 2P + g and runs its
+//    MFMAs in 2P + g + 1): W of a stage is last read in phase q1, A rows of group g in q2, so
+//    k-tile j + 2 may refill stage j & 1 from slot 8j + 5 (W) / 8j + 6 (A rows of group 0) /
+//    8j + 7 (group 1); every issuing wave waits for its pieces before the barrier that opens
+//    the first read of that k-tile (the end of slot 8j + 7 for k-tile j + 1).
+#include <type_traits>
+
+#include "common.h"
+
+namespace clipvit {
+
+// v[i] += bias[i] for the lane's 16 contiguous features (bias staged in LDS)
+__device__ __forceinline__ void colv_add16(float (&v)[16], const float* bias) {
+    const float4* b4 = (const float4*)bias;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float4 bb = b4[i];
+        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
+    }
+}
+
+template <typename T, int EPI, int SM>
+__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
+    typedef typename T::vec8 vec8;
+    constexpr int BM = 256, BN = 256;
+    constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;  // 64 KB per 64-deep k-tile
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + BN * 4];
+    float* const colv = (float*)(smem + 2 * STAGE);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int nN = a.N / BN;
+    int mt, nt;
+    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, nN, a.xcd_n, mt, nt)) return;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const size_t ldb = (size_t)a.K * 2;
+    const int nk = a.K >> 6;  // even, >= 2 (launcher)
+
+    // ---- staging: group 0 fills A (32 pieces of 8 rows x 128 B), group 1 fills W. Part p (0..3)
+    // of a k-tile = pieces 8p + 2 wc + {0, 1} of the group's operand (one phase's issue).
+    const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
+    const int r0 = grp == 0 ? m0 : n0, rows = grp == 0 ? a.M : a.N;
+    const size_t opbytes = (size_t)(rows - r0) * ldb;
+    const i32x4_t rs = buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(opbytes < 0xFFFFFFFFu ? opbytes : 0xFFFFFFFFu));
+    const int lr = lane >> 3, chunk = (lane & 7) ^ lr;  // piece rows are 8-aligned: row & 7 = lr
+    unsigned voff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
+        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);  // rows past M / N: out of range -> 0
+    }
+    const int opbase = grp == 0 ? 0 : A_BYTES;
+    auto issue = [&](int part, int j) {
+        if (j >= nk) return;
+        unsigned char* dst = smem + (j & 1) * STAGE + opbase;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int pc = 8 * part + 2 * wc + i;
+            blds16(rs, voff[2 * part + i], j * 128, dst + pc * 1024);
+        }
+    };
+
+    // epilogue bias: one column per thread, loaded now, parked in LDS at the end
+    float cb = 0.f;
+    if (tid < BN && a.bias) cb = a.bias[n0 + tid];
+
+    f32x4 acc[4][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- prologue: k-tile 0 whole, then what the steady state issues before phase q0 of k-tile 0
+    // (group 0: part 0 of k-tile 1 at q3(-1); group 1: parts 0, 1 of k-tile 1 at q2(-1), q3(-1))
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue(p, 0);
+    if (grp == 0) {
+        issue(0, 1);
+        vm_wait<2>();
+    } else {
+        issue(0, 1);
+        issue(1, 1);
+        vm_wait<4>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
+    const int aoff = (grp * 128 + lrow) * 128, woff = A_BYTES + (wc * 64 + lrow) * 128;
+    const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;  // k-halves 0 / 1
+    vec8 af[4][2], wf[4][2];
+
+    // one k-tile (4 phases) on stage S
+    auto ktile = [&](const int kt, const unsigned char* st) {
+        // q0: A rows 0-63 of the wave's half, W features 0-31
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
+            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f][0] = *(const vec8*)(st + aoff + f * 2048 + c0);
+            af[f][1] = *(const vec8*)(st + aoff + f * 2048 + c1);
+        }
+        if (grp == 0) issue(1, kt + 1); else issue(2, kt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q1: W features 32-63 (last W read of this stage)
+#pragma unroll
+        for (int f = 2; f < 4; ++f) {
+            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
+            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
+        }
+        if (grp == 0) issue(2, kt + 1); else issue(3, kt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 2; fn < 4; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q2: A rows 64-127 (last A read of this stage); W of k-tile kt + 2 may refill it now
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c0);
+            af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c1);
+        }
+        if (grp == 0) issue(3, kt + 1); else issue(0, kt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 2; fn < 4; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm + 4]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q3: no reads (W features 0-31 still in registers); the A rows of group 0 may refill
+        if (grp == 0) {
+            issue(0, kt + 2);
+        } else {
+            issue(1, kt + 2);
+            // W of k-tile kt + 1 landed before group 0 reads it (next slot)
+            if (kt + 2 < nk) vm_wait<4>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm) acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm + 4]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 0) {  // A of k-tile kt + 1 landed before its first read
+            if (kt + 2 < nk) vm_wait<2>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+    };
+
+    for (int kt = 0; kt < nk; kt += 2) {
+        ktile(kt, smem);
+        ktile(kt + 1, smem + STAGE);
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: group 1's last MFMAs done
+
+    // ---- epilogue: bias (LDS), optional QuickGELU, 16-bit stores ----
+    constexpr bool GELU = EPI == EPI_GELU;
+    if (tid < BN) colv[tid] = cb;
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    const int g = lg;
+    if constexpr (SM == 3) {
+        // row-contiguous stores staged through the (now free) LDS ring, as gemm.hip SM = 3
+        constexpr int ROWB = BN * 2, CPR = ROWB / 16;
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm) {
+            const int r = grp * 128 + fm * 16 + lrow;
+            const int nl = wc * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+            colv_add16(v, colv + nl);
+            if constexpr (GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+            }
+            const int cc = nl >> 3;
+            unsigned char* rowp = smem + r * ROWB;
+            *(uint4*)(rowp + (((cc) ^ (r & 7)) << 4)) =
+                make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+            *(uint4*)(rowp + (((cc + 1) ^ (r & 7)) << 4)) =
+                make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        unsigned char* Cb = (unsigned char*)a.C;
+#pragma unroll 4
+        for (int i = tid; i < BM * CPR; i += 512) {
+            const int r = i / CPR, c = i % CPR;
+            const int m = m0 + r;
+            const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
+            if (m < a.M) *(uint4*)(Cb + ((size_t)m * a.ldc + n0) * 2 + c * 16) = val;
+        }
+    } else {
+        unsigned char* Cb = (unsigned char*)a.C;
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm) {
+            const int m = m0 + grp * 128 + fm * 16 + lrow;
+            if (m >= a.M) continue;
+            const int nl = wc * 64 + 16 * g;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+            colv_add16(v, colv + nl);
+            if constexpr (GELU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+            }
+            const size_t off = ((size_t)m * a.ldc + n0 + nl) * 2;
+            *(uint4*)(Cb + off) =
+                make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+            *(uint4*)(Cb + off + 16) =
+                make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent form (variant 62): one workgroup per CU walks the tiles blockIdx.x, blockIdx.x + G,
+// ... (G = grid size; logical ids through the same bijective XCD remap, so every XCD group
+// keeps a contiguous range of the row-major tile order each round). The k-tile stream runs on
+// across tile boundaries: the last phases of a tile already stage the next tile's first two
+// k-tiles, so a tile's prologue load never stalls the CU, and the finished tile's epilogue
+// (bias, QuickGELU, 16-bit stores straight from the accumulators) runs in the first read
+// segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
+// whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
+template <typename T, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
+    typedef typename T::vec8 vec8;
+    constexpr int BM = 256, BN = 256;
+    constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+    constexpr int NBIAS = 8192;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 160 KB
+    float* const colv = (float*)(smem + 2 * STAGE);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int nM = (a.M + BM - 1) / BM, nN = a.N / BN;
+    const int G = gridDim.x;
+    const size_t ldb = (size_t)a.K * 2;
+    const int nk = a.K >> 6;  // even, >= 2
+
+    auto tile = [&](int i, int& m0, int& n0) {
+        const int L = blockIdx.x + i * G;
+        if (L >= ntiles) return false;
+        int mt, nt;
+        tile_of_block(L, nM, nN, a.xcd_n, mt, nt);
+        m0 = mt * BM;
+        n0 = nt * BN;
+        return true;
+    };
+    const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
+    const int rows = grp == 0 ? a.M : a.N;
+    auto rsrc_of = [&](int m0, int n0) {
+        const int r0 = grp == 0 ? m0 : n0;
+        const size_t bytes = (size_t)(rows - r0) * ldb;
+        return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
+    };
+    const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
+    unsigned voff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
+        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
+    }
+    const int opbase = grp == 0 ? 0 : A_BYTES;
+
+    int m0, n0, mn = 0, nn = 0;
+    tile(0, m0, n0);  // the launcher sizes the grid <= ntiles
+    bool has_next = tile(1, mn, nn);
+    i32x4_t rs_c = rsrc_of(m0, n0), rs_n = has_next ? rsrc_of(mn, nn) : rs_c;
+    // k-tile j of the current tile's frame (j >= nk: k-tile j - nk of the next tile)
+    auto issue = [&](int part, int j) {
+        i32x4_t r = rs_c;
+        int kk = j;
+        if (j >= nk) {
+            if (!has_next) return;
+            r = rs_n;
+            kk = j - nk;
+        }
+        unsigned char* dst = smem + (j & 1) * STAGE + opbase;  // nk even: the stream's parity
+#pragma unroll
+        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * 128, dst + (8 * part + 2 * wc + i) * 1024);
+    };
+
+    f32x4 acc[4][8];
+    // prologue (as gemm_pp_kernel)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue(p, 0);
+    if (grp == 0) {
+        issue(0, 1);
+    } else {
+        issue(0, 1);
+        issue(1, 1);
+    }
+    // the bias vector -> LDS (ordinary loads: the compiler drains vmcnt before the LDS writes,
+    // which only waits for the prologue pieces a little early)
+    for (int i = tid; i < a.N; i += 512) colv[i] = a.bias ? a.bias[i] : 0.f;
+    if (grp == 0) vm_wait<2>(); else vm_wait<4>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (a.pp_delay > 0) {  // fewer tiles than the busiest workgroups: start late (see GemmArgs)
+        const int mine = (ntiles - 1 - (int)blockIdx.x) / G + 1, most = (ntiles - 1) / G + 1;
+        if (mine < most) {
+            const int n = a.pp_delay * (int)((blockIdx.x >> 3) & 3);
+            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+        }
+    }
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
+    const int aoff = (grp * 128 + lrow) * 128, woff = A_BYTES + (wc * 64 + lrow) * 128;
+    const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;
+    vec8 af[4][2], wf[4][2];
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+
+    // one k-tile (4 phases); Z: the tile's first k-tile (k-half 0 MFMAs start from zero)
+    auto ktile = [&](const int kt, const unsigned char* st, auto Zc) {
+        constexpr bool Z = decltype(Zc)::value;
+        const bool more = kt + 2 < nk || has_next;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
+            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f][0] = *(const vec8*)(st + aoff + f * 2048 + c0);
+            af[f][1] = *(const vec8*)(st + aoff + f * 2048 + c1);
+        }
+        if (grp == 0) issue(1, kt + 1); else issue(2, kt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int f = 2; f < 4; ++f) {
+            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
+            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
+        }
+        if (grp == 0) issue(2, kt + 1); else issue(3, kt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 2; fn < 4; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c0);
+            af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c1);
+        }
+        if (grp == 0) issue(3, kt + 1); else issue(0, kt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 2; fn < 4; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm + 4]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        if (grp == 0) {
+            issue(0, kt + 2);
+        } else {
+            issue(1, kt + 2);
+            if (more) vm_wait<4>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int fn = 0; fn < 2; ++fn)
+#pragma unroll
+                for (int fm = 0; fm < 4; ++fm)
+                    acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm + 4]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 0) {
+            if (more) vm_wait<2>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+    };
+
+    constexpr bool GELU = EPI == EPI_GELU;
+    unsigned char* const Cb = (unsigned char*)a.C;
+    for (int i = 1;; ++i) {
+        ktile(0, smem, std::true_type{});
+        ktile(1, smem + STAGE, std::false_type{});
+        for (int kt = 2; kt < nk; kt += 2) {
+            ktile(kt, smem, std::false_type{});
+            ktile(kt + 1, smem + STAGE, std::false_type{});
+        }
+        // epilogue of this tile: the other group is in its MFMA segment meanwhile. The lane's 16
+        // bias values come from LDS by inline-asm reads: a plain LDS read here makes hipcc drain
+        // vmcnt(0) first (the next tile's staging DMA may alias it, as far as it knows)
+        const int n = n0 + wc * 64 + 16 * lg;
+        f32x4 bv[4];
+        {
+            const unsigned ba = (unsigned)(size_t)(LDS_AS const float*)(colv + n);
+            asm volatile("ds_read_b128 %0, %1" : "=v"(bv[0]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(bv[1]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(bv[2]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(bv[3]) : "v"(ba) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm) {
+            const int m = m0 + grp * 128 + fm * 16 + lrow;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
+            if constexpr (GELU) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+            }
+#if CLIPVIT_ABLATE == 3  // diagnostic build only: no epilogue stores (values kept live)
+            if (m < a.M && a.ldc > (1 << 30)) {
+#else
+            if (m < a.M) {
+#endif
+                const size_t off = ((size_t)m * a.ldc + n) * 2;
+                *(uint4*)(Cb + off) =
+                    make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
+                *(uint4*)(Cb + off + 16) = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                                      pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+            }
+        }
+        if (!has_next) break;
+        m0 = mn;
+        n0 = nn;
+        rs_c = rs_n;
+        has_next = tile(i + 1, mn, nn);
+        if (has_next) rs_n = rsrc_of(mn, nn);
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+}
+
+template <typename T>
+static int launch_pp_t(hipStream_t s, int epi, const GemmArgs& a, int sm) {
+    const int nwg = grid_for((a.M + 255) / 256, a.N / 256, a.xcd_n);
+#define PP(E, S) gemm_pp_kernel<T, E, S><<<nwg, 512, 0, s>>>(a)
+    if (epi == EPI_STORE) { if (sm == 3) PP(EPI_STORE, 3); else PP(EPI_STORE, 0); return 0; }
+    if (epi == EPI_GELU) { if (sm == 3) PP(EPI_GELU, 3); else PP(EPI_GELU, 0); return 0; }
+#undef PP
+    return -1;
+}
+
+template <typename T>
+static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
+    static const int ncu = [] {
+        int d = 0, n = 0;
+        (void)hipGetDevice(&d);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+        return n > 0 ? n : 256;
+    }();
+    const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = ntiles < ncu ? ntiles : ncu;
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    return -1;
+}
+
+// variant 60: direct stores from the accumulators; 61: LDS-staged row-contiguous stores;
+// 62: persistent (direct stores; 1-D XCD maps only, N <= 8192)
+int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
+    if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
+    if (variant == 62) {
+        if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
+        return dtype == 2 ? launch_ppp_t<F16>(s, epi, a) : launch_ppp_t<BF16>(s, epi, a);
+    }
+    const int sm = variant == 61 ? 3 : 0;
+    return dtype == 2 ? launch_pp_t<F16>(s, epi, a, sm) : launch_pp_t<BF16>(s, epi, a, sm);
+}
+
+}  // namespace clipvit
