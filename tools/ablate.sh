@@ -2,7 +2,9 @@
 # Diagnostic builds of the library (CPU side, this container): ab/noload.so (GEMM operand fill
 # removed: MFMAs on stale LDS) and ab/nomfma.so (GEMM MFMAs removed: fill, barriers and
 # epilogue only). Outputs are garbage; only the GEMM family times mean anything. Compare with
-# tools/ab_multi.sh "<args>" R CLIPVIT_LIB=$PWD/ab/noload.so CLIPVIT_LIB=$PWD/ab/nomfma.so -
+# tools/ab_envs.sh "<args>" R - CLIPVIT_LIB=$PWD/ab/noload.so CLIPVIT_LIB=$PWD/ab/nomfma.so
+# (CLIPVIT_ABLATE=3, no epilogue stores in the persistent ping-pong GEMM, is built the same way
+# for gemm_pp.hip alone: DESIGN.md §5.8.)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p ab/abl1 ab/abl2

@@ -11,4 +11,4 @@ if [ "$1" != "nontest" ]; then
 fi
 timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.log
-if [ "$1" = "prof" ] || [ "$2" = "prof" ]; then bash tools/profile_round.sh gpurun_out/prof && echo prof-ok; fi
+if [ "$1" = "prof" ] || [ "$2" = "prof" ]; then bash tools/profile_round.sh gpurun_out/prof r03 && echo prof-ok; fi

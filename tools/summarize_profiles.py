@@ -165,7 +165,7 @@ def main():
     flops = {r: 2 * m * n * k for r, (m, n, k) in shapes.items()}
     # algorithmic bytes per launch: A once, W once, 16-bit C once
     algo = {r: 2 * (m * k + n * k + m * n) for r, (m, n, k) in shapes.items()}
-    lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16; {lane_b} images per launch)", "",
+    lines = [f"# {tag}: rocprofv3 summary of `python bench.py` (ViT-B/32, bs 256, fp16 MFMA operands, fp32 pixels; {lane_b} images per launch)", "",
              "avg us / TFLOP/s: isolated dispatches (bench.py's serialised profile pass, what its roofline",
              "times); concurrent us: the timed loop's dispatches, two lanes sharing the GPU. TFLOP/s = the",
              "launch's own FLOPs / isolated average. Algorithmic MB = A + W + C (16-bit) once. PMC MB =",
@@ -199,6 +199,12 @@ def main():
     entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
              "mlp_gemm_avg_us": sum(t["avg_us"] for t in mlp) / len(mlp), "source": f"profiles/{tag}_summary.md",
              "note": "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reports half of wide streaming reads); Infinity-Cache hits are included by the counters"}
+    if "fc" in traffic:  # bench.py --traffic-json: the dominant kernel's own PMC bytes per launch
+        t = traffic["fc"]
+        (prof / f"{tag}_fc_traffic.json").write_text(json.dumps({
+            "fc_gemm_bytes_per_launch": t["read_bytes"] + t["write_bytes"], "fc_gemm_avg_us": t["avg_us"],
+            "fc_gemm_algorithmic_bytes": algo["fc"] + algo.get("fc_tail", 0),
+            "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)"}, indent=1))
     pj = prof / "pmc_traffic.json"
     data = json.loads(pj.read_text()) if pj.exists() else {}
     entry["images_per_launch"] = lane_b
