@@ -158,8 +158,9 @@ struct clipvit_handle {
     // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
     // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
-    // 2,388 (same-box A/B). CLIPVIT_LARGE_VARIANTS="q,f"
-    int large_var[2] = {3462, 3462};
+    // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
+    // family 7.49 -> 7.03 ms per L/14 lane forward. CLIPVIT_LARGE_VARIANTS="q,f"
+    int large_var[2] = {3462, 3463};
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -1306,7 +1307,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 60 ||
-                        variant == 61 || variant == 62;
+                        variant == 61 || variant == 62 || variant == 63;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

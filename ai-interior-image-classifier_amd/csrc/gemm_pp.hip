@@ -285,7 +285,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // (bias, QuickGELU, 16-bit stores straight from the accumulators) runs in the first read
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
-template <typename T, int EPI>
+template <typename T, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -513,10 +513,16 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             if (m < a.M) {
 #endif
                 const size_t off = ((size_t)m * a.ldc + n) * 2;
-                *(uint4*)(Cb + off) =
-                    make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
-                *(uint4*)(Cb + off + 16) = make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
-                                                      pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
+                const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+                const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
+                                  pack2<T>(v[14], v[15])};
+                if constexpr (NT) {  // non-temporal: no L2 allocation for the output (A/B, §5.8)
+                    __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
+                    __builtin_nontemporal_store(w1, (u32x4*)(Cb + off + 16));
+                } else {
+                    *(u32x4*)(Cb + off) = w0;
+                    *(u32x4*)(Cb + off + 16) = w1;
+                }
             }
         }
         if (!has_next) break;
@@ -539,7 +545,7 @@ static int launch_pp_t(hipStream_t s, int epi, const GemmArgs& a, int sm) {
     return -1;
 }
 
-template <typename T>
+template <typename T, bool NT>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     static const int ncu = [] {
         int d = 0, n = 0;
@@ -549,18 +555,19 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     }();
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
 // variant 60: direct stores from the accumulators; 61: LDS-staged row-contiguous stores;
-// 62: persistent (direct stores; 1-D XCD maps only, N <= 8192)
+// 62: persistent (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with non-temporal stores
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
-    if (variant == 62) {
+    if (variant == 62 || variant == 63) {
         if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-        return dtype == 2 ? launch_ppp_t<F16>(s, epi, a) : launch_ppp_t<BF16>(s, epi, a);
+        if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
+        return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     }
     const int sm = variant == 61 ? 3 : 0;
     return dtype == 2 ? launch_pp_t<F16>(s, epi, a, sm) : launch_pp_t<BF16>(s, epi, a, sm);
