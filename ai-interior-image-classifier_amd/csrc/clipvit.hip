@@ -159,8 +159,8 @@ struct clipvit_handle {
     // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
     // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
-    // family 7.49 -> 7.03 ms per L/14 lane forward. CLIPVIT_LARGE_VARIANTS="q,f"
-    int large_var[2] = {3462, 3463};
+    // family 7.49 -> 7.03 ms per L/14 lane forward. CLIPVIT_LARGE_VARIANTS="q,f[,o,p]"
+    int large_var[4] = {3462, 3463, 0, 0};  // QKV, c_fc, out_proj, c_proj
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -411,7 +411,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     if (!h->var_forced && role != R_PATCH &&
         (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu))) {
         variant = epi == EPI_GELU ? 8 : 80;
-        const int lv = role == R_QKV ? h->large_var[0] : role == R_FC ? h->large_var[1] : 0;
+        const int lv = role == R_QKV ? h->large_var[0] : role == R_FC ? h->large_var[1]
+                     : role == R_OUT ? h->large_var[2] : role == R_PROJ ? h->large_var[3] : 0;
         if (lv && (epi == EPI_STORE || epi == EPI_GELU)) {
             a.xcd_n = lv / 100;
             variant = lv % 100;
@@ -952,9 +953,13 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
             h->ncu = ncu;
     }
-    if (const char* v = getenv("CLIPVIT_LARGE_VARIANTS")) {
-        h->large_var[0] = atoi(v);
-        if (const char* c = strchr(v, ',')) h->large_var[1] = atoi(c + 1);
+    if (const char* v = getenv("CLIPVIT_LARGE_VARIANTS")) {  // "q,f[,o,p]"
+        int k = 0;
+        for (const char* p = v; *p && k < 4; ++k) {
+            h->large_var[k] = atoi(p);
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
     }
     if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
         h->var_forced = true;
