@@ -159,8 +159,9 @@ struct clipvit_handle {
     // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
     // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
-    // family 7.49 -> 7.03 ms per L/14 lane forward. CLIPVIT_LARGE_VARIANTS="q,f[,o,p]"
-    int large_var[4] = {3462, 3463, 0, 0};  // QKV, c_fc, out_proj, c_proj
+    // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
+    // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). CLIPVIT_LARGE_VARIANTS="q,f[,o,p]"
+    int large_var[4] = {3462, 3463, 3463, 3463};  // QKV, c_fc, out_proj, c_proj
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -198,8 +199,11 @@ struct clipvit_handle {
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
     // whole-round row split of the 16-bit-output GEMMs (see gemm()); off by default since c_fc
     // runs on the 160x128 tile (var above); CLIPVIT_GEMM_SPLIT=1 enables
-    bool round_split = false;
-    int split_main = 8, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
+    // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
+    // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
+    // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
+    bool round_split = true;
+    int split_main = 62, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
     // XCD map of the main launch (tile_of_block; CLIPVIT_SPLIT_XCD): 34 = the 1-D remap over a
     // column-group-major order with 2 N-groups, so each XCD group keeps half of W (2.4 MB of
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
@@ -393,6 +397,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             GemmArgs b = a;
             b.M = (int)m1;
             b.xcd_n = h->split_xcd;  // 1-D bijective remap (whole rounds per XCD group)
+            if (h->split_main >= 60 && xcd_split_n(N / 256, b.xcd_n)) b.xcd_n = 0;  // ping-pong: 1-D maps only
             GemmArgs c = a;
             c.A = (const unsigned char*)A + (size_t)m1 * K * 2;
             c.C = (unsigned char*)C + (size_t)m1 * ldc * 2;
@@ -907,7 +912,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
         const int m = atoi(v);
-        if (m == 8 || m == 80) h->split_main = m;
+        if (m == 8 || m == 80 || (m >= 60 && m <= 63)) h->split_main = m;
         if (const char* c = strchr(v, ',')) h->split_tail = atoi(c + 1);
     }
     if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
