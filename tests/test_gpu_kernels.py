@@ -214,3 +214,22 @@ def test_attention_tail_rows_never_read(gpu, B, N, H, causal):
     ref = _ref_attention(qkv, B, N, H, causal=causal)
     err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 3e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
+                                   (36928 // 4, 4096, 1024)])
+def test_ping_pong_race_screen(gpu, M, N, K):
+    """The ping-pong GEMMs (60, 61, 62, 63) hand LDS stages between waves by counted vmcnt and
+    barriers only. Every accumulator sees the same k order as the 2-phase 256x256 tile (v8), so
+    the outputs must equal v8's bit for bit on every one of many repeated launches: a read that
+    overtook its DMA (or a refill that overtook a read) would show as a differing tile."""
+    g = torch.Generator(device=gpu).manual_seed(M + N)
+    A = torch.randn(M, K, device=gpu, generator=g).to(torch.float16)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(N, device=gpu, generator=g)
+    for epi in (10, 11):  # 16-bit store / QuickGELU
+        ref = E.gemm_test(A, W, bias, epi=epi, variant=8)
+        for variant in (60, 61, 62, 63, 3462):
+            for _ in range(6):
+                C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
+                assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
