@@ -175,7 +175,7 @@ struct clipvit_handle {
     bool mx8 = false;
     // MX-fp8 GEMM tile per role (qkv, out, fc, proj); CLIPVIT_MX8_VARIANTS. 128x128 everywhere:
     // measured at M = 25,600 (bs 512) qkv 88 -> 80 us, c_fc 110 -> 103 us against 128x256
-    int var8[4] = {2, 2, 2, 2};
+    int var8[4] = {3, 2, 2, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
     // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
@@ -468,7 +468,9 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.bias = bias; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     if (epi == EPI_GELU_Q8) a.sC = (unsigned char*)C + (size_t)M * N;
     a.xcd_n = h->xcd[role];
-    if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, h->var8[role]) != 0 &&
+    const int v8 = h->var8[role];
+    if ((v8 == 3 || v8 == 4) && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
+    if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, v8) != 0 &&
         launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, 0) != 0) {
         g_err = "gemm8: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
                 " K=" + std::to_string(K);

@@ -403,13 +403,341 @@ static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
     return 0;
 }
 
-// variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves)
+// ---------------------------------------------------------------------------------------
+// Ping-pong MX-fp8 tile (variants 3 persistent / 4 one tile per workgroup): gemm_ppp_kernel's
+// schedule (gemm_pp.hip) at BK = 128 fp8. A k-tile row is 128 B in both
+// formats, so the LDS layout, the staging pieces and the phase/slot plan are the 16-bit
+// kernel's; per phase a wave runs 8 scaled 16x16x128 MFMAs (2x the cycles of the 16-bit form,
+// so the same matrix-pipe time per phase as the 16 bf16 MFMAs it replaces). Each stage also
+// carries the 4 scale bytes of every A and W row (2 KB): the wave that issues part 0 of its
+// group's operand stages the scale dwords of 64 rows with one 4-byte buffer_load ... lds, so
+// part 0 is 3 VMEM ops and the counted waits are 3 (group 0) / 5 (group 1). Scale rows are
+// read with their fragments (A: q0, q2; W: q0, q1) and refilled with part 0 (group 1 at q2,
+// group 0 at q3), after the last read of each.
+template <typename TO, int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int ntiles) {
+    constexpr int BM = 256, BN = 256;
+    constexpr int A_BYTES = BM * 128, OPS = (BM + BN) * 128, STAGE = OPS + (BM + BN) * 4;  // 66 KB
+    constexpr int NBIAS = 4096;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 148 KB
+    float* const colv = (float*)(smem + 2 * STAGE);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, wc = wave & 3;
+    const int nM = (a.M + BM - 1) / BM, nN = a.N / BN;
+    const int G = gridDim.x;
+    const size_t ldb = (size_t)a.K, lds_ = (size_t)(a.K / 32);
+    const int nk = a.K >> 7;  // even, >= 2 (launcher)
+
+    auto tile = [&](int i, int& m0, int& n0) {
+        const int L = blockIdx.x + i * G;
+        if (L >= ntiles) return false;
+        int mt, nt;
+        tile_of_block(L, nM, nN, a.xcd_n, mt, nt);
+        m0 = mt * BM;
+        n0 = nt * BN;
+        return true;
+    };
+    const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
+    const unsigned char* ssrc = grp == 0 ? a.sA : a.sW;
+    const int rows = grp == 0 ? a.M : a.N;
+    auto rsrc_of = [&](int m0, int n0) {
+        const int r0 = grp == 0 ? m0 : n0;
+        const size_t bytes = (size_t)(rows - r0) * ldb;
+        return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
+    };
+    // scale dwords: one resource over the whole scale array (rows past M / N read 0), the
+    // tile's row offset in the per-lane offset (VGPRs: the SGPR budget is spent)
+    const i32x4_t ssr = buf_rsrc(ssrc, (unsigned)((size_t)rows * lds_));
+    auto svoff_of = [&](int m0, int n0) { return (unsigned)(((grp == 0 ? m0 : n0) + wc * 64 + lane) * lds_); };
+    const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
+    unsigned voff[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
+        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
+    }
+    const unsigned obase = (grp == 0 ? 0 : A_BYTES) + 2 * wc * 1024;  // + (8 part + i) KB
+    const unsigned sbase = OPS + grp * BM * 4 + wc * 256;
+
+    int m0, n0, mn = 0, nn = 0;
+    tile(0, m0, n0);  // the launcher sizes the grid <= ntiles
+    bool has_next = tile(1, mn, nn);
+    i32x4_t rs_c = rsrc_of(m0, n0), rs_n = has_next ? rsrc_of(mn, nn) : rs_c;
+    unsigned sv_c = svoff_of(m0, n0), sv_n = has_next ? svoff_of(mn, nn) : sv_c;
+    // k-tile j of the current tile's frame (j >= nk: k-tile j - nk of the next tile)
+    // S: the stage k-tile j lands in (= j & 1, nk even), a compile-time constant at every call
+    // so that the LDS destinations are immediates (m0), not SGPRs
+    auto issue = [&](int part, int j, auto S) {
+        i32x4_t r = rs_c;
+        unsigned sv = sv_c;
+        int kk = j;
+        if (j >= nk) {
+            if (!has_next) return;
+            r = rs_n;
+            sv = sv_n;
+            kk = j - nk;
+        }
+        // the wave's LDS offsets, opaque per call: otherwise the compiler hoists all 18 m0
+        // values of the loop into SGPRs and spills (the destinations stay smem-based pointers,
+        // which keeps the fragment ds_reads free of compiler-inserted vmcnt(0))
+        unsigned ob = obase, sb = sbase;
+        asm volatile("" : "+s"(ob), "+s"(sb));
+        constexpr unsigned so = decltype(S)::value * STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * 128, smem + ob + so + (8 * part + i) * 1024);
+        if (part == 0) raw_buffer_load_lds(ssr, (LDS_AS void*)(smem + sb + so), 4, (int)sv, kk * 4, 0, 0);
+    };
+
+    f32x4 acc[4][8];
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) issue(p, 0, S0{});
+    if (grp == 0) {
+        issue(0, 1, S1{});
+    } else {
+        issue(0, 1, S1{});
+        issue(1, 1, S1{});
+    }
+    for (int i = tid; i < a.N; i += 512) colv[i] = a.bias ? a.bias[i] : 0.f;
+    if (grp == 0) vm_wait<3>(); else vm_wait<5>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+    // lane-derived LDS read addresses: re-derived per tile from an opaque lane id (asm, so
+    // neither it nor they are loop-invariant). Held across the whole persistent loop they
+    // get spilled, and their reload at a tile's first read waits for every staging load.
+    auto lane_id = [] {
+        int l;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+        return l;
+    };
+    int aoff, woff, asoff, wsoff, c0, c1, sshift;
+    auto lane_addrs = [&] {
+        const int l = lane_id();
+        const int lrow = l & 15, lsw = l & 7, lg = l >> 4;
+        aoff = (grp * 128 + lrow) * 128;
+        woff = A_BYTES + (wc * 64 + lrow) * 128;
+        asoff = OPS + (grp * 128 + lrow) * 4;
+        wsoff = OPS + BM * 4 + (wc * 64 + lrow) * 4;
+        c0 = ((0 | lg) ^ lsw) << 4;
+        c1 = ((4 | lg) ^ lsw) << 4;
+        sshift = 8 * lg;  // the lane's scale byte (k-block lg) within the row's dword
+    };
+    i32x8 af[4], wf[4];
+    int as[4], ws[4];
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    // fragment and scale reads through non-char types: with char / unsigned-int typed LDS reads
+    // the compiler cannot tell them apart from the pending LDS-DMA writes and puts vmcnt(0) in
+    // front of every read phase (the 16-bit kernel's bf16x8 reads do not have that problem)
+    auto frag = [&](const unsigned char* p) -> i32x8 {
+        const i32x4_t lo = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + c0));
+        const i32x4_t hi = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + c1));
+        return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    };
+    auto scale = [&](const unsigned char* p) -> int {
+        return (int)((__builtin_bit_cast(unsigned, *(const float*)p) >> sshift) & 0xffu);
+    };
+    auto mfmas = [&](auto FN0, auto FM0, auto Zc) {
+        constexpr int fn0 = decltype(FN0)::value, fm0 = decltype(FM0)::value;
+#pragma unroll
+        for (int fn = fn0; fn < fn0 + 2; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm)
+                acc[fn][fm + fm0] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                    wf[fn], af[fm], decltype(Zc)::value ? zero : acc[fn][fm + fm0], 0, 0, 0, ws[fn], 0, as[fm]);
+        // pin the block to its phase: the MFMA intrinsics are pure, and without a use here IR
+        // sinking moves them past the barriers (into the next phases' read segments)
+#pragma unroll
+        for (int fn = fn0; fn < fn0 + 2; ++fn)
+#pragma unroll
+            for (int fm = 0; fm < 4; ++fm) asm volatile("" : "+v"(acc[fn][fm + fm0]));
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    using I4 = std::integral_constant<int, 4>;
+
+    auto ktile = [&](const int kt, auto Pc, auto Zc) {
+        constexpr int P = decltype(Pc)::value;  // kt & 1
+        using PS = std::integral_constant<int, P>;
+        using NS = std::integral_constant<int, P ^ 1>;
+        const unsigned char* st = smem + P * STAGE;
+        const bool more = kt + 2 < nk || has_next;
+        // q0: W features 0-31, A rows 0-63 of the wave's half
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+            wf[f] = frag(st + woff + f * 2048);
+            ws[f] = scale(st + wsoff + f * 64);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f] = frag(st + aoff + f * 2048);
+            as[f] = scale(st + asoff + f * 64);
+        }
+        if (grp == 0) issue(1, kt + 1, NS{}); else issue(2, kt + 1, NS{});
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(I0{}, I0{}, Zc);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q1: W features 32-63 (last W read of this stage)
+#pragma unroll
+        for (int f = 2; f < 4; ++f) {
+            wf[f] = frag(st + woff + f * 2048);
+            ws[f] = scale(st + wsoff + f * 64);
+        }
+        if (grp == 0) issue(2, kt + 1, NS{}); else issue(3, kt + 1, NS{});
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(I2{}, I0{}, Zc);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q2: A rows 64-127 (last A read of this stage)
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+            af[f] = frag(st + aoff + (f + 4) * 2048);
+            as[f] = scale(st + asoff + (f + 4) * 64);
+        }
+        if (grp == 0) issue(3, kt + 1, NS{}); else issue(0, kt + 2, PS{});
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(I2{}, I4{}, Zc);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        // q3: no reads
+        if (grp == 0) {
+            issue(0, kt + 2, PS{});
+        } else {
+            issue(1, kt + 2, PS{});
+            if (more) vm_wait<5>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(I0{}, I4{}, Zc);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 0) {
+            if (more) vm_wait<3>(); else vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();
+    };
+
+    for (int i = 1;; ++i) {
+        lane_addrs();
+        ktile(0, S0{}, std::true_type{});
+        ktile(1, S1{}, std::false_type{});
+        for (int kt = 2; kt < nk; kt += 2) {
+            ktile(kt, S0{}, std::false_type{});
+            ktile(kt + 1, S1{}, std::false_type{});
+        }
+        // epilogue (as gemm_ppp_kernel: bias from LDS by inline-asm reads, no vmcnt drain). The
+        // lane coordinates are re-derived from an opaque, recomputed lane id: loop-invariant
+        // epilogue addresses hoisted out of the persistent loop get spilled (the k-loop holds
+        // 255 VGPRs), and a scratch reload here would wait for the next tile's staging loads
+        const int ln = lane_id();
+        const int er = ln & 15, eg = ln >> 4;
+        const int n = n0 + wc * 64 + 16 * eg;
+        f32x4 bv[4];
+        {
+            const unsigned ba = (unsigned)(size_t)(LDS_AS const float*)(colv + n);
+            asm volatile("ds_read_b128 %0, %1" : "=v"(bv[0]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(bv[1]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(bv[2]) : "v"(ba) : "memory");
+            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(bv[3]) : "v"(ba) : "memory");
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm) {
+            const int m = m0 + grp * 128 + fm * 16 + er;
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
+            if constexpr (EPI == EPI_GELU_Q8) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                // MX block = 32 features = this lane's 16 + those of lane ^ 16 (same token):
+                // ds_swizzle bitmask mode, xor 0x10 within 32-lane groups (no address VGPR)
+                float am = 0.f;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) am = fmaxf(am, fabsf(v[q]));
+                am = fmaxf(am, __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(am), 0x401F)));
+                const int e = mx_exp(am);
+                const float inv = mx_inv(e);
+                if (m < a.M) {
+                    *(uint4*)((unsigned char*)a.C + (size_t)m * a.ldc + n) =
+                        make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
+                                   pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
+                                   pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
+                                   pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
+                    if ((eg & 1) == 0) a.sC[(size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
+                }
+            } else if (m < a.M) {  // EPI_STORE
+                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
+                dst[0] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                    pack2<TO>(v[6], v[7]));
+                dst[1] = make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]), pack2<TO>(v[12], v[13]),
+                                    pack2<TO>(v[14], v[15]));
+            }
+        }
+        if (!has_next) break;
+        m0 = mn;
+        n0 = nn;
+        rs_c = rs_n;
+        sv_c = sv_n;
+        has_next = tile(i + 1, mn, nn);
+        if (has_next) {
+            rs_n = rsrc_of(mn, nn);
+            sv_n = svoff_of(mn, nn);
+        }
+    }
+    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+}
+
+template <typename TO>
+static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persistent) {
+    if (a.N % 256 || a.K % 256 || a.N > 4096 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
+    static const int ncu = [] {
+        int d = 0, n = 0;
+        (void)hipGetDevice(&d);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
+        return n > 0 ? n : 256;
+    }();
+    const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+    const int grid = persistent && ntiles > ncu ? ncu : ntiles;
+    if (epi == EPI_STORE) { gemm_mx8_pp_kernel<TO, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU_Q8) { gemm_mx8_pp_kernel<TO, EPI_GELU_Q8><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    return -1;
+}
+
+// variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves), 3 ping-pong 256x256
+// persistent, 4 ping-pong 256x256 one tile per workgroup
 template <typename TO>
 static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
     if (variant == 0) variant = a.N % 256 == 0 ? 1 : 2;
     switch (variant) {
         case 1: return launch_mx8_tile<TO, 128, 256, 2, 4>(s, epi, a);
         case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
+        case 3: return launch_mx8_pp<TO>(s, epi, a, true);
+        case 4: return launch_mx8_pp<TO>(s, epi, a, false);
     }
     return -1;
 }

@@ -109,6 +109,26 @@ def test_gemm_mx8_vs_dequantized_reference(gpu, variant, M, N, K):
     assert err < 1e-4, err
 
 
+@pytest.mark.parametrize("variant", [3, 4])
+@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
+                                   (700, 768, 3072), (257, 512, 256)])
+def test_gemm_mx8_ping_pong_bit_identical(gpu, variant, M, N, K):
+    """The 256x256 ping-pong MX tile (3 persistent, 4 one tile per workgroup) accumulates every
+    output in the same k order as the 128x256 tile: its bf16 store and its MX-fp8 (QuickGELU)
+    output must be bit-identical to variant 1's, over repeated launches (race screen, as
+    test_gpu_kernels.py's ping-pong screen)."""
+    A8, sA, W, bias, Ad, Wd = _quantized_operands(gpu, M, N, K, M + N + K + 1)
+    ref5 = E.gemm_mx8_test(A8, sA, W, bias, epi=5, variant=1)
+    ref4 = E.gemm_mx8_test(A8, sA, W, bias, epi=4, variant=1)
+    ref = torch.from_numpy(Ad @ Wd.T).float() + bias.cpu()[None, :]
+    assert ((ref5.cpu().float() - ref).abs().max() / ref.abs().max()).item() < 1e-2
+    for rep in range(3):
+        got5 = E.gemm_mx8_test(A8, sA, W, bias, epi=5, variant=variant)
+        assert torch.equal(got5, ref5), (rep, (got5.float() - ref5.float()).abs().max().item())
+        q, s = E.gemm_mx8_test(A8, sA, W, bias, epi=4, variant=variant)
+        assert torch.equal(s, ref4[1]) and torch.equal(q, ref4[0]), rep
+
+
 def test_gemm_mx8_exact_integers(gpu):
     """Small integers are exact in e4m3 under any scale: C must equal the integer product."""
     M, N, K = 256, 512, 384

@@ -5,8 +5,11 @@
 For every shape, each round times every variant once (clipvit_gemm_bench: `iters` back-to-back
 launches on random uniform operands, HIP events), rounds alternate the variant order; prints the
 median and min per variant in us and TF/s. epi = internal Epi enum (0 store16, 1 gelu16).
+GEMM_AB_DTYPE selects the operand format (1 bf16; 2 fp16, default; 3 MX-fp8, where epi 1 runs
+as the MX-fp8 QuickGELU output).
 """
 import ctypes
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -22,12 +25,13 @@ variants = [int(v) for v in sys.argv[2].split(",")]
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 iters = int(sys.argv[4]) if len(sys.argv) > 4 else 20
 L = _lib.lib()
+dtype = int(os.environ.get("GEMM_AB_DTYPE", "2"))
 for M, N, K, epi in shapes:
     t = {v: [] for v in variants}
     for r in range(rounds):
         for v in (variants if r % 2 == 0 else variants[::-1]):
             ms = ctypes.c_float()
-            if t[v] is not None and L.clipvit_gemm_bench(2, M, N, K, epi, v, iters, ctypes.byref(ms)) == 0:
+            if t[v] is not None and L.clipvit_gemm_bench(dtype, M, N, K, epi, v, iters, ctypes.byref(ms)) == 0:
                 t[v].append(ms.value * 1e3)
             else:
                 t[v] = None
