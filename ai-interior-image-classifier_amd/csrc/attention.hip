@@ -186,9 +186,15 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // registers, so more workgroups per CU hide the load latency.
 // CAUSAL (text tower): key j masked for query i < j; key blocks past the workgroup's last query
 // are neither loaded nor computed.
-template <typename T, int QW = 4, bool SINGLE = false, bool CAUSAL = false>
+// Q8 (MX-fp8 forward): the output goes straight to the out_proj operand format instead of 16-bit
+// `out`: each value rounded to T first, then quantized by the launch_quant_mx8 rule, so the bytes
+// equal attention + quant_mx8 exactly. MX block b of a head = features 32 b .. 32 b + 31 = the
+// lane's dt 2b, 2b+1 values across the 4 lanes of its query (g = 0..3).
+template <typename T, int QW = 4, bool SINGLE = false, bool CAUSAL = false, bool Q8 = false>
 __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(const u16* __restrict__ qkv,
-                                                                                u16* __restrict__ out, int N, int H) {
+                                                                                u16* __restrict__ out, int N, int H,
+                                                                                unsigned char* __restrict__ q8 = nullptr,
+                                                                                unsigned char* __restrict__ q8s = nullptr) {
     typedef typename T::vec8 vec8;
     constexpr int STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
     __shared__ __attribute__((aligned(16))) unsigned char smem[(SINGLE ? 1 : 2) * STAGE];
@@ -331,7 +337,36 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
 
     l_run += __shfl_xor(l_run, 16, 64);
     l_run += __shfl_xor(l_run, 32, 64);
-    if (q < N) {
+    if constexpr (Q8) {
+        const float inv = 1.0f / l_run;
+        float v[4][4], am[2] = {0.f, 0.f};
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 4; r += 2) {
+                const unsigned w = pack2<T>(o[dt][r] * inv, o[dt][r + 1] * inv);
+                v[dt][r] = T::to_f32((u16)(w & 0xffff));
+                v[dt][r + 1] = T::to_f32((u16)(w >> 16));
+                am[dt >> 1] = fmaxf(am[dt >> 1], fmaxf(fabsf(v[dt][r]), fabsf(v[dt][r + 1])));
+            }
+#pragma unroll
+        for (int bk = 0; bk < 2; ++bk) {
+            am[bk] = fmaxf(am[bk], __shfl_xor(am[bk], 16, 64));
+            am[bk] = fmaxf(am[bk], __shfl_xor(am[bk], 32, 64));
+        }
+        if (q < N) {
+            const int e0 = mx_exp(am[0]), e1 = mx_exp(am[1]);
+            const float i0 = mx_inv(e0), i1 = mx_inv(e1);
+            unsigned char* qrow8 = q8 + (base + q) * D + h * 64;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const float iv = dt < 2 ? i0 : i1;
+                *(unsigned*)(qrow8 + dt * 16 + 4 * g) =
+                    pk4_e4m3(v[dt][0] * iv, v[dt][1] * iv, v[dt][2] * iv, v[dt][3] * iv);
+            }
+            if (g < 2) q8s[(base + q) * (D / 32) + h * 2 + g] = (unsigned char)((g == 0 ? e0 : e1) + 127);
+        }
+    } else if (q < N) {
         const float inv = 1.0f / l_run;
         u16* orow = out + (base + q) * D + h * 64;
 #pragma unroll
@@ -552,6 +587,19 @@ static bool attn_v2() {
         return !v || atoi(v) != 0;
     }();
     return on;
+}
+
+// attention with the output quantized to MX-fp8 (q8 [B N, D] e4m3 + q8s [B N, D / 32] scales) in
+// the kernel, for the shapes that run on the one-key-block attention_v2 (N <= 64: ViT-B/32);
+// returns -1 otherwise (the caller then runs launch_attention + launch_quant_mx8, the same bytes)
+int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,
+                        int B, int N, int H) {
+    if (!attn_v2() || N > 64 || attn_v3() >= 2) return -1;
+    dim3 grid(1, H, B), block(256);
+    const u16* in = (const u16*)qkv;
+    if (dtype == 2) attention_v2_kernel<F16, 4, true, false, true><<<grid, block, 0, s>>>(in, nullptr, N, H, q8, q8s);
+    else attention_v2_kernel<BF16, 4, true, false, true><<<grid, block, 0, s>>>(in, nullptr, N, H, q8, q8s);
+    return 0;
 }
 
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,

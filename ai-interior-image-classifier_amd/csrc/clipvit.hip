@@ -202,6 +202,9 @@ struct clipvit_handle {
     // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
     // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
     // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
+    // MX-fp8 forward: attention writes the out_proj operand (MX-fp8) itself instead of 16-bit
+    // output + launch_quant_mx8 (same bytes; CLIPVIT_ATTN_Q8=0 restores the two kernels)
+    bool attn_q8 = true;
     bool round_split = true;
     int split_main = 62, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
     // XCD map of the main launch (tile_of_block; CLIPVIT_SPLIT_XCD): 34 = the 1-D remap over a
@@ -570,8 +573,10 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
                : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV);
         if (rc) return rc;
         if (prof) prof->mark(s, F_QKV);
-        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
-        if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
+        if (!q || !h->attn_q8 || launch_attention_q8(s, h->dt, w->qkv, q8, q8s, B, N, h->cfg.heads) != 0) {
+            launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+            if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
+        }
         if (prof) prof->mark(s, F_ATTN);
         if (last && h->cls_prune && !q) {  // bf16 last block: class-token rows only
             if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
@@ -912,6 +917,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         h->lnfold = h->resid16 && h->dt == CLIPVIT_F16 && h->D <= 1024 && atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_ATTN_Q8")) h->attn_q8 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
         const int m = atoi(v);
         if (m == 8 || m == 80 || (m >= 60 && m <= 63)) h->split_main = m;

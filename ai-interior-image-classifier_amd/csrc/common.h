@@ -335,6 +335,8 @@ void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* s
                         const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D);
 
 
+int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,
+                        int B, int N, int H);
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal = false);
 

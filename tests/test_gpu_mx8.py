@@ -256,3 +256,27 @@ def test_mxfp8_forward_variants(gpu, monkeypatch, model, skip, resid16):
     finally:
         e16.close()
         e8.close()
+
+
+def test_attention_q8_output_bit_identical(gpu, monkeypatch):
+    """The MX-fp8 forward's attention writes the out_proj operand (MX-fp8) in its epilogue
+    (ViT-B/32, N = 50): embeddings and logits must equal those of the two-kernel path
+    (16-bit attention output + launch_quant_mx8, CLIPVIT_ATTN_Q8=0) bit for bit."""
+    cfg = C.get_config("ViT-B/32")
+    sd = synthetic_state_dict(cfg, 0)
+    adapters = synthetic_adapters(cfg, rank=8)
+    g = torch.Generator().manual_seed(91)
+    segs = [0, 40, 60, 359, 395, 425, 437]
+    B = 24
+    px = torch.randn(B, 3, 224, 224, generator=g).clamp_(-1.8, 2.2).to(gpu)
+    T = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
+    fused = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B)
+    monkeypatch.setenv("CLIPVIT_ATTN_Q8", "0")
+    split = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B)
+    try:
+        a, b = fused.classify(px), split.classify(px)
+        assert torch.equal(a.emb, b.emb)
+        assert torch.equal(a.logits, b.logits)
+    finally:
+        fused.close()
+        split.close()
