@@ -76,6 +76,7 @@ struct Lane {
     float* f = nullptr;  // [cap, E] projected features
     float2* st = nullptr;  // lnfold: [cap*N, D/128] per-row 128-column (mean, M2) of x
     unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
+    void* x16 = nullptr;  // MX-fp8 mode: [cap*N, D] fp16 residual stream (handle x16)
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
 };
@@ -202,6 +203,14 @@ struct clipvit_handle {
     // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
     // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
     // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
+    // MX-fp8 forward, fp16 residual stream: the residual x lives in fp16 between the LayerNorm
+    // kernels (which add and normalise in fp32) instead of fp32, halving their x bytes
+    // (LayerNorm family = 30 % fewer HBM bytes). Needs the deferred 16-bit branch path and a
+    // 16-bit class-token tail (the tail widens the class rows to fp32). CLIPVIT_X16=0: fp32 x.
+    bool x16 = true;
+    bool use_x16() const {
+        return x16 && mx8 && resid16 && defer_x && cls_prune && ((mx8_skip >> (cfg.layers - 1)) & 1);
+    }
     // MX-fp8 forward: attention writes the out_proj operand (MX-fp8) itself instead of 16-bit
     // output + launch_quant_mx8 (same bytes; CLIPVIT_ATTN_Q8=0 restores the two kernels)
     bool attn_q8 = true;
@@ -255,6 +264,7 @@ static int free_ws(Workspace* w) {
         hipFree(l.f);
         hipFree(l.st);
         hipFree(l.q8);
+        hipFree(l.x16);
         if (l.done) hipEventDestroy(l.done);
         if (l.stream) hipStreamDestroy(l.stream);
     }
@@ -284,6 +294,7 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess) e = hipMalloc((void**)&l.f, (size_t)l.cap * h->E * sizeof(float));
         if (e == hipSuccess && h->lnfold) e = hipMalloc((void**)&l.st, rows * (h->D / 128) * sizeof(float2));
         if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
+        if (e == hipSuccess && h->mx8) e = hipMalloc(&l.x16, rows * h->D * 2);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
     }
@@ -488,7 +499,8 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
 // and of the attention output are gathered into compact [B, D] buffers carved from u (dead
 // here); the arithmetic per row is the same kernels' (bit-identical result, tests/
 // test_gpu_parity.py::test_cls_prune_is_bit_identical).
-static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof) {
+static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof,
+                    const void* x16 = nullptr) {
     const int D = h->D, N = h->N;
     const LayerW& ly = h->layers[h->cfg.layers - 1];
     unsigned char* base = (unsigned char*)w->u;
@@ -498,7 +510,7 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     // split-K partial products: the full-M qkv buffer is dead once gather_cls has run
     // (S * B * 4D * 4 bytes <= B * N * 3D * 2 for S <= 8, N >= 50)
     float* part = (float*)w->qkv;
-    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D);
+    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D, x16);
     // M = B rows: 64x64 tiles alone give B/64 x N/64 workgroups whose K-long dependency chains
     // (48 k-tiles for c_proj) bound the tail, so each GEMM splits K into S slices (fixed per
     // shape: results do not depend on B) summed in slice order by the following kernel.
@@ -543,6 +555,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
     unsigned char* q8s = q8 + (size_t)M * D;
     unsigned char* u8 = (unsigned char*)w->u;
     int rc;
+    void* X16 = h->use_x16() ? w->x16 : nullptr;  // fp16 residual stream (nullptr: fp32 x)
     auto ln = [&](const float* g, const float* b, bool q) {
         if (q) launch_layernorm_q8(s, w->x, q8, q8s, g, b, M, D);
         else launch_layernorm(s, h->dt, w->x, w->h, g, b, M, D);
@@ -550,19 +563,19 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
     // x (+)= y (+ y2), then LayerNorm into the next GEMM's operand format. yb = y2: x = (x + y) + y2
     // stored; yb null: x + y, stored unless defer
     auto add_ln = [&](const void* ya, const void* yb, const float* g, const float* b, bool q, bool defer) {
-        if (q) launch_add_layernorm_q8(s, w->x, ya, yb, q8, q8s, g, b, M, D, defer);
-        else if (yb || defer) launch_add_layernorm_deferred(s, h->dt, w->x, ya, yb, w->h, g, b, M, D);
-        else launch_add_layernorm(s, h->dt, w->x, ya, w->h, g, b, M, D);
+        if (q) launch_add_layernorm_q8(s, w->x, ya, yb, q8, q8s, g, b, M, D, defer, X16);
+        else if (yb || defer) launch_add_layernorm_deferred(s, h->dt, w->x, ya, yb, w->h, g, b, M, D, X16);
+        else launch_add_layernorm(s, h->dt, w->x, ya, w->h, g, b, M, D, X16);
     };
     if (prof) prof->mark(s, F_EMBED);
     if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
     if (h->q8_layer(0))
         launch_embed_ln_q8(s, w->x, q8, q8s, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
-                           l0.ln1b, B, N, D);
+                           l0.ln1b, B, N, D, X16);
     else
         launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
-                        l0.ln1b, B, N, D);
+                        l0.ln1b, B, N, D, X16);
     if (prof) prof->mark(s, F_EMBED);
     void* y = w->qkv;
     void* y2 = (u16*)w->qkv + (size_t)M * D;
@@ -579,7 +592,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         }
         if (prof) prof->mark(s, F_ATTN);
         if (last && h->cls_prune && !q) {  // bf16 last block: class-token rows only
-            if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
+            if ((rc = cls_tail(h, s, B, w, f_out, prof, X16))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
         }
@@ -918,6 +931,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_ATTN_Q8")) h->attn_q8 = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_X16")) h->x16 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
         const int m = atoi(v);
         if (m == 8 || m == 80 || (m >= 60 && m <= 63)) h->split_main = m;

@@ -301,8 +301,9 @@ void launch_quant_mx8(hipStream_t s, int in_dtype, const void* src, unsigned cha
 void launch_fill_random_mx8(hipStream_t s, unsigned char* q, unsigned char* sq, size_t n, unsigned seed);
 void launch_pack_weight_mx8(hipStream_t s, const float* src, unsigned char* q, unsigned char* sq,
                             int N, int K, int Kp);
+// x16 (here and below): the fp16 residual stream of the MX-fp8 forward replaces fp32 x (nullptr: x)
 void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
-                          const float* b, int rows, int D);
+                          const float* b, int rows, int D, void* x16 = nullptr);
 // x' = x + y (+ y2); h = LayerNorm(x'). y2 == nullptr: x' is NOT stored (deferred: the next
 // call adds both branch outputs in the same order); y2 != nullptr: x' is stored.
 // split-K reduction of the class-token tail (cls_tail): t = P[0] + ... + P[S-1] (fixed order),
@@ -313,16 +314,20 @@ void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, 
 void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const float* bias, void* u, int rows,
                         int n);
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
-                                   void* h, const float* g, const float* b, int rows, int D);
-void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D);
+                                   void* h, const float* g, const float* b, int rows, int D, void* x16 = nullptr);
+void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
+                       const void* x16 = nullptr);
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,
                          const float* g, const float* b, int rows, int D);
 // x (+)= y (+ y2), LayerNorm -> MX-fp8 q + scales sq (bf16 branch outputs of the MX-fp8 forward)
 void launch_add_layernorm_q8(hipStream_t s, float* x, const void* y, const void* y2, unsigned char* q,
-                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer);
+                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer,
+                             void* x16 = nullptr);
+// x16 given: x holds the patch GEMM's fp32 rows (read only), the residual goes to x16 (fp16)
 void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,
                         const float* cls, const float* pos, const float* g_pre,
-                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D);
+                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D,
+                        void* x16 = nullptr);
 
 void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_t n);
 // LayerNorm fold of a Linear (W [N, K] fp32, possibly LoRA-merged): Wg = W diag(gamma) (fp32,
@@ -342,7 +347,7 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D);
+                     const float* b1, int B, int N, int D, void* x16 = nullptr);
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
                       const float* b, int rows, int D);
 void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,

@@ -114,6 +114,20 @@ void launch_cast_pixels(hipStream_t s, int in_dtype, int out_dtype, const void* 
 // ---------------------------------------------------------------------------------------
 // Row LayerNorm helpers ln_row / store_row16: common.h (shared with text.hip).
 
+// fp16 residual rows (X16): lane's float4 slices <-> 4 fp16 values each
+template <int V>
+__device__ __forceinline__ void store_x16(u16* xr, float4 (&v)[V], int lane) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const uint2 w = make_uint2(pack2<F16>(v[i].x, v[i].y), pack2<F16>(v[i].z, v[i].w));
+        *(uint2*)(xr + (lane + 64 * i) * 4) = w;
+    }
+}
+__device__ __forceinline__ float4 unpack4_f16(uint2 w) {
+    return make_float4(F16::to_f32((u16)(w.x & 0xffff)), F16::to_f32((u16)(w.x >> 16)),
+                       F16::to_f32((u16)(w.y & 0xffff)), F16::to_f32((u16)(w.y >> 16)));
+}
+
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
 // E8M0 scale (rule: common.h mx_exp).
@@ -136,7 +150,9 @@ __device__ __forceinline__ void store_row_q8(unsigned char* q, unsigned char* sq
 
 // x[row] = ln_pre((t == 0 ? class_embedding : patch_row) + pos[t]);  h[row] = ln_1(x[row])
 // (Q8: h as MX-fp8 q [rows][D] + scales sq [rows][D/32])
-template <typename T, int V, bool Q8 = false>
+// X16 (MX-fp8 forward, fp16 residual stream): x holds the patch GEMM's fp32 rows (read only) and
+// the residual goes to x16 as fp16.
+template <typename T, int V, bool Q8 = false, bool X16 = false>
 __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, void* __restrict__ h,
                                                        unsigned char* __restrict__ sq,
                                                        const float* __restrict__ cls,
@@ -145,7 +161,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
                                                        const float* __restrict__ bp,
                                                        const float* __restrict__ g1,
                                                        const float* __restrict__ b1, int rows,
-                                                       int N) {
+                                                       int N, u16* __restrict__ x16) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -162,8 +178,12 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
         v[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
     }
     ln_row<V>(v, gp, bp, lane, (float)D);
+    if constexpr (X16) {
+        store_x16<V>(x16 + (size_t)row * D, v, lane);
+    } else {
 #pragma unroll
-    for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+        for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    }
     ln_row<V>(v, g1, b1, lane, (float)D);
     if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v, lane);
     else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
@@ -273,8 +293,10 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // Moves the residual add out of the GEMM epilogue (which then only stores y): the GEMM no
 // longer reads x, and this kernel streams x, y -> x, h in one pass.
 // Q8: h is the MX-fp8 A operand of the next GEMM (q [rows][D] + E8M0 scales sq [rows][D/32]).
-template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false>
-__global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ x, const u16* __restrict__ y,
+// X16: x is the fp16 residual stream (u16 storage) instead of fp32; the sum and the LayerNorm are
+// fp32, the stored x is its fp16 rounding.
+template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false>
+__global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ xv, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
                                                             const float* __restrict__ gm,
@@ -285,6 +307,8 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
     if (row0 >= rows) return;
     constexpr int D = 256 * V;
+    float* const x = (float*)xv;
+    u16* const x16 = (u16*)xv;
     float4 v[RPW][V];
     uint2 w[RPW][V], w2[RPW][V];
 #pragma unroll
@@ -294,7 +318,8 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
         const u16* yr = y + (size_t)row * D;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
-            v[r][i] = *(const float4*)(xr + (lane + 64 * i) * 4);
+            if constexpr (X16) v[r][i] = unpack4_f16(*(const uint2*)(x16 + (size_t)row * D + (lane + 64 * i) * 4));
+            else v[r][i] = *(const float4*)(xr + (lane + 64 * i) * 4);
             w[r][i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
             if constexpr (TWO) w2[r][i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
         }
@@ -317,8 +342,9 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(float* __restrict__ 
                 v[r][i].z += T::to_f32((u16)(w2[r][i].y & 0xffff));
                 v[r][i].w += T::to_f32((u16)(w2[r][i].y >> 16));
             }
-            if constexpr (STORE_X) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
+            if constexpr (STORE_X && !X16) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
         }
+        if constexpr (STORE_X && X16) store_x16<V>(x16 + (size_t)row * D, v[r], lane);
         ln_row<V>(v[r], gm, bt, lane, (float)D);
         if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v[r], lane);
         else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
@@ -401,22 +427,27 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D) {
+                     const float* b1, int B, int N, int D, void* x16) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
+    u16* xo = (u16*)x16;
     if (dtype == 2) {
-        DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+        if (xo) DISPATCH_V(D, embed_ln_kernel<F16, V, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        else DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, nullptr))
     } else {
-        DISPATCH_V(D, embed_ln_kernel<BF16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+        if (xo) DISPATCH_V(D, embed_ln_kernel<BF16, V, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        else DISPATCH_V(D, embed_ln_kernel<BF16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, nullptr))
     }
 }
 
 void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char* sq,
                         const float* cls, const float* pos, const float* g_pre,
-                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D) {
+                        const float* b_pre, const float* g1, const float* b1, int B, int N, int D, void* x16) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
-    DISPATCH_V(D, embed_ln_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, cls, pos, g_pre, b_pre, g1, b1, rows, N));
+    u16* xo = (u16*)x16;
+    if (xo) DISPATCH_V(D, embed_ln_kernel<BF16, V, true, true><<<grid, block, 0, s>>>(x, q, sq, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+    else DISPATCH_V(D, embed_ln_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, cls, pos, g_pre, b_pre, g1, b1, rows, N, nullptr))
 }
 
 void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* st, const float* cls,
@@ -442,37 +473,46 @@ void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsign
     DISPATCH_V(D, layernorm_kernel<BF16, V, true><<<grid, block, 0, s>>>(x, q, sq, g, b, rows));
 }
 
-void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
-                          const float* b, int rows, int D) {
+template <typename T, int V, bool X16>
+static void add_ln_plain(hipStream_t s, void* x, const u16* y, void* h, const float* g, const float* b, int rows) {
     dim3 grid((rows + 3) / 4), block(256);
+    add_layernorm_kernel<T, V, true, false, 1, false, X16><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+}
+void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, void* h, const float* g,
+                          const float* b, int rows, int D, void* x16) {
+    const u16* yy = (const u16*)y;
     if (dtype == 2) {
-        DISPATCH_V(D, add_layernorm_kernel<F16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, h, nullptr, g, b, rows));
+        if (x16) DISPATCH_V(D, add_ln_plain<F16, V, true>(s, x16, yy, h, g, b, rows))
+        else DISPATCH_V(D, add_ln_plain<F16, V, false>(s, x, yy, h, g, b, rows))
     } else {
-        DISPATCH_V(D, add_layernorm_kernel<BF16, V><<<grid, block, 0, s>>>(x, (const u16*)y, nullptr, h, nullptr, g, b, rows));
+        if (x16) DISPATCH_V(D, add_ln_plain<BF16, V, true>(s, x16, yy, h, g, b, rows))
+        else DISPATCH_V(D, add_ln_plain<BF16, V, false>(s, x, yy, h, g, b, rows))
     }
 }
 
-template <typename T, int V>
-static void add_ln_deferred(hipStream_t s, float* x, const u16* y, const u16* y2, u16* h, const float* g,
+template <typename T, int V, bool X16>
+static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
     dim3 grid((rows + 3) / 4), block(256);
-    if (y2) add_layernorm_kernel<T, V, true, true><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
-    else add_layernorm_kernel<T, V, false, false><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+    if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+    else add_layernorm_kernel<T, V, false, false, 1, false, X16><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
 }
 
 // MX-fp8 forms (bf16 branch outputs): y2 given -> x = (x + y) + y2 stored; y2 null -> x + y not
 // stored when defer (the add after out_proj), stored otherwise; LayerNorm -> q8 + scales
-template <int V>
-static void add_ln_q8(hipStream_t s, float* x, const u16* y, const u16* y2, unsigned char* q, unsigned char* sq,
+template <int V, bool X16>
+static void add_ln_q8(hipStream_t s, void* x, const u16* y, const u16* y2, unsigned char* q, unsigned char* sq,
                       const float* g, const float* b, int rows, bool defer) {
     dim3 grid((rows + 3) / 4), block(256);
-    if (y2) add_layernorm_kernel<BF16, V, true, true, 1, true><<<grid, block, 0, s>>>(x, y, y2, q, sq, g, b, rows);
-    else if (defer) add_layernorm_kernel<BF16, V, false, false, 1, true><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
-    else add_layernorm_kernel<BF16, V, true, false, 1, true><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
+    if (y2) add_layernorm_kernel<BF16, V, true, true, 1, true, X16><<<grid, block, 0, s>>>(x, y, y2, q, sq, g, b, rows);
+    else if (defer) add_layernorm_kernel<BF16, V, false, false, 1, true, X16><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
+    else add_layernorm_kernel<BF16, V, true, false, 1, true, X16><<<grid, block, 0, s>>>(x, y, nullptr, q, sq, g, b, rows);
 }
 void launch_add_layernorm_q8(hipStream_t s, float* x, const void* y, const void* y2, unsigned char* q,
-                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer) {
-    DISPATCH_V(D, add_ln_q8<V>(s, x, (const u16*)y, (const u16*)y2, q, sq, g, b, rows, defer));
+                             unsigned char* sq, const float* g, const float* b, int rows, int D, bool defer,
+                             void* x16) {
+    if (x16) DISPATCH_V(D, add_ln_q8<V, true>(s, x16, (const u16*)y, (const u16*)y2, q, sq, g, b, rows, defer))
+    else DISPATCH_V(D, add_ln_q8<V, false>(s, x, (const u16*)y, (const u16*)y2, q, sq, g, b, rows, defer))
 }
 
 void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, int S, const float* bias,
@@ -498,32 +538,39 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
 }
 
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
-                                   void* h, const float* g, const float* b, int rows, int D) {
+                                   void* h, const float* g, const float* b, int rows, int D, void* x16) {
+    const u16 *yy = (const u16*)y, *yy2 = (const u16*)y2;
     if (dtype == 2) {
-        DISPATCH_V(D, add_ln_deferred<F16, V>(s, x, (const u16*)y, (const u16*)y2, (u16*)h, g, b, rows));
+        if (x16) DISPATCH_V(D, add_ln_deferred<F16, V, true>(s, x16, yy, yy2, (u16*)h, g, b, rows))
+        else DISPATCH_V(D, add_ln_deferred<F16, V, false>(s, x, yy, yy2, (u16*)h, g, b, rows))
     } else {
-        DISPATCH_V(D, add_ln_deferred<BF16, V>(s, x, (const u16*)y, (const u16*)y2, (u16*)h, g, b, rows));
+        if (x16) DISPATCH_V(D, add_ln_deferred<BF16, V, true>(s, x16, yy, yy2, (u16*)h, g, b, rows))
+        else DISPATCH_V(D, add_ln_deferred<BF16, V, false>(s, x, yy, yy2, (u16*)h, g, b, rows))
     }
 }
 
 // CLS rows of a [B*N, D] token buffer pair -> compact [B, D] buffers (x fp32, h 16-bit):
 // the last block's row-wise ops (out_proj, LayerNorm, MLP) only matter for the class token,
 // which is all that ln_post(x[:, 0, :]) @ proj reads.
-__global__ __launch_bounds__(256) void gather_cls_kernel(const float* __restrict__ x, const u16* __restrict__ h,
+// (X16: x is the fp16 residual stream; xc receives its fp32 widening)
+template <bool X16>
+__global__ __launch_bounds__(256) void gather_cls_kernel(const void* __restrict__ x, const u16* __restrict__ h,
                                                          float* __restrict__ xc, u16* __restrict__ hc, int N,
                                                          int D, int B) {
     const int b = blockIdx.x;
     if (b >= B) return;
-    const float* xs = x + (size_t)b * N * D;
     const u16* hs = h + (size_t)b * N * D;
     for (int c = threadIdx.x * 4; c < D; c += 1024) {
-        *(float4*)(xc + (size_t)b * D + c) = *(const float4*)(xs + c);
+        if constexpr (X16) *(float4*)(xc + (size_t)b * D + c) = unpack4_f16(*(const uint2*)((const u16*)x + (size_t)b * N * D + c));
+        else *(float4*)(xc + (size_t)b * D + c) = *(const float4*)((const float*)x + (size_t)b * N * D + c);
         *(uint2*)(hc + (size_t)b * D + c) = *(const uint2*)(hs + c);
     }
 }
 
-void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D) {
-    gather_cls_kernel<<<B, 256, 0, s>>>(x, (const u16*)h, xc, (u16*)hc, N, D, B);
+void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
+                       const void* x16) {
+    if (x16) gather_cls_kernel<true><<<B, 256, 0, s>>>(x16, (const u16*)h, xc, (u16*)hc, N, D, B);
+    else gather_cls_kernel<false><<<B, 256, 0, s>>>(x, (const u16*)h, xc, (u16*)hc, N, D, B);
 }
 
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
