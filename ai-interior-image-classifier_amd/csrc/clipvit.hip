@@ -181,7 +181,12 @@ struct clipvit_handle {
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
     // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
     uint64_t mx8_skip = 0;
-    bool q8_layer(int i) const { return mx8 && !((mx8_skip >> i) & 1); }
+    // blocks whose MLP (c_fc, c_proj) stays bf16: the attention roles (QKV, out_proj) follow
+    // mx8_skip, the MLP roles this mask (CLIPVIT_MX8_SKIP sets both, CLIPVIT_MX8_SKIP_MLP this one):
+    // the MLP GEMMs carry most of the MX-fp8 error, QKV / out_proj little of it
+    uint64_t mx8_skip_mlp = 0;
+    bool q8_attn(int i) const { return mx8 && !((mx8_skip >> i) & 1); }
+    bool q8_mlp(int i) const { return mx8 && !((mx8_skip_mlp >> i) & 1); }
     // residual adds of out_proj / c_proj: true = the GEMM stores its 16-bit branch output y and
     // the following LayerNorm kernel does x += y (fp16 and bf16 default; CLIPVIT_RESID16=0/1 overrides);
     // false = fp32 read-modify-write of x in the GEMM epilogue
@@ -208,8 +213,14 @@ struct clipvit_handle {
     // (LayerNorm family = 30 % fewer HBM bytes). Needs the deferred 16-bit branch path and a
     // 16-bit class-token tail (the tail widens the class rows to fp32). CLIPVIT_X16=0: fp32 x.
     bool x16 = true;
+    // 16-bit forward (fp16 / bf16), 24-bit residual stream: x between the LayerNorm kernels as
+    // 16 + 8 bit planes (norm.hip x24_load) instead of fp32: the add + LayerNorm kernels move 3
+    // bytes per element of x instead of 4 (CLIPVIT_X24=0: fp32 x)
+    bool x24 = true;
+    bool use_x24() const { return x24 && !mx8 && !lnfold && resid16 && defer_x && cls_prune; }
     bool use_x16() const {
-        return x16 && mx8 && resid16 && defer_x && cls_prune && ((mx8_skip >> (cfg.layers - 1)) & 1);
+        return x16 && mx8 && resid16 && defer_x && cls_prune && ((mx8_skip >> (cfg.layers - 1)) & 1) &&
+               ((mx8_skip_mlp >> (cfg.layers - 1)) & 1);
     }
     // MX-fp8 forward: attention writes the out_proj operand (MX-fp8) itself instead of 16-bit
     // output + launch_quant_mx8 (same bytes; CLIPVIT_ATTN_Q8=0 restores the two kernels)
@@ -295,6 +306,7 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess && h->lnfold) e = hipMalloc((void**)&l.st, rows * (h->D / 128) * sizeof(float2));
         if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
         if (e == hipSuccess && h->mx8) e = hipMalloc(&l.x16, rows * h->D * 2);
+        else if (e == hipSuccess && h->use_x24()) e = hipMalloc(&l.x16, rows * h->D * 3);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
     }
@@ -500,7 +512,7 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
 // here); the arithmetic per row is the same kernels' (bit-identical result, tests/
 // test_gpu_parity.py::test_cls_prune_is_bit_identical).
 static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof,
-                    const void* x16 = nullptr) {
+                    const void* x16 = nullptr, bool x24 = false) {
     const int D = h->D, N = h->N;
     const LayerW& ly = h->layers[h->cfg.layers - 1];
     unsigned char* base = (unsigned char*)w->u;
@@ -510,7 +522,7 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     // split-K partial products: the full-M qkv buffer is dead once gather_cls has run
     // (S * B * 4D * 4 bytes <= B * N * 3D * 2 for S <= 8, N >= 50)
     float* part = (float*)w->qkv;
-    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D, x16);
+    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D, x16, x24);
     // M = B rows: 64x64 tiles alone give B/64 x N/64 workgroups whose K-long dependency chains
     // (48 k-tiles for c_proj) bound the tail, so each GEMM splits K into S slices (fixed per
     // shape: results do not depend on B) summed in slice order by the following kernel.
@@ -570,7 +582,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
     if (prof) prof->mark(s, F_EMBED);
     if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
-    if (h->q8_layer(0))
+    if (h->q8_attn(0))
         launch_embed_ln_q8(s, w->x, q8, q8s, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g,
                            l0.ln1b, B, N, D, X16);
     else
@@ -581,7 +593,8 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
     void* y2 = (u16*)w->qkv + (size_t)M * D;
     for (int i = 0; i < h->cfg.layers; ++i) {
         const LayerW& ly = h->layers[i];
-        const bool q = h->q8_layer(i), last = i + 1 == h->cfg.layers;
+        // q: the attention roles (QKV, out_proj) in MX-fp8; qm: the MLP roles
+        const bool q = h->q8_attn(i), qm = h->q8_mlp(i), last = i + 1 == h->cfg.layers;
         rc = q ? gemm8(s, h, EPI_STORE, q8, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)
                : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV);
         if (rc) return rc;
@@ -591,7 +604,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
             if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
         }
         if (prof) prof->mark(s, F_ATTN);
-        if (last && h->cls_prune && !q) {  // bf16 last block: class-token rows only
+        if (last && h->cls_prune && !q && !qm) {  // bf16 last block: class-token rows only
             if ((rc = cls_tail(h, s, B, w, f_out, prof, X16))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
@@ -603,24 +616,24 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
                : gemm(s, h, eo, w->h, ly.wout, ly.bout, co, M, D, D, D, R_OUT);
         if (rc) return rc;
         if (prof) prof->mark(s, F_OUT);
-        if (r16) add_ln(y, nullptr, ly.ln2g, ly.ln2b, q, defer);
-        else ln(ly.ln2g, ly.ln2b, q);
+        if (r16) add_ln(y, nullptr, ly.ln2g, ly.ln2b, qm, defer);
+        else ln(ly.ln2g, ly.ln2b, qm);
         if (prof) prof->mark(s, F_LN);
-        rc = q ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
+        rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
                : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC);
         if (rc) return rc;
         if (prof) prof->mark(s, F_FC);
         const bool p16 = r16 && !last;
         const int ep = p16 ? EPI_STORE : EPI_RESID;
         void* cp = p16 ? (defer ? y2 : y) : (void*)w->x;
-        rc = q ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ)
+        rc = qm ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ)
                : gemm(s, h, ep, w->u, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ);
         if (rc) return rc;
         if (prof) prof->mark(s, F_PROJ);
         if (!last) {
             const LayerW& nx = h->layers[i + 1];
-            if (p16) add_ln(y, defer ? y2 : nullptr, nx.ln1g, nx.ln1b, h->q8_layer(i + 1), false);
-            else ln(nx.ln1g, nx.ln1b, h->q8_layer(i + 1));
+            if (p16) add_ln(y, defer ? y2 : nullptr, nx.ln1g, nx.ln1b, h->q8_attn(i + 1), false);
+            else ln(nx.ln1g, nx.ln1b, h->q8_attn(i + 1));
             if (prof) prof->mark(s, F_LN);
         }
     }
@@ -734,8 +747,10 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     if (prof) prof->mark(s, F_EMBED);
     if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
     const LayerW& l0 = h->layers[0];
+    // X24: the residual stream in 24-bit planes (w->x then only holds the patch GEMM's rows)
+    void* X24 = h->use_x24() ? w->x16 : nullptr;
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
-                    B, N, D);
+                    B, N, D, X24, X24 != nullptr);
     if (prof) prof->mark(s, F_EMBED);
     // 16-bit residual branch outputs (resid16) reuse the qkv buffer: qkv is dead once attention
     // has read it. y = out_proj's branch, y2 = c_proj's. With deferred adds (defer_x), the add
@@ -753,7 +768,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (prof) prof->mark(s, F_ATTN);
         if (last && h->cls_prune) {
-            if ((rc = cls_tail(h, s, B, w, f_out, prof))) return rc;
+            if ((rc = cls_tail(h, s, B, w, f_out, prof, X24, X24 != nullptr))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
         }
@@ -761,7 +776,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         if (h->resid16) {
             if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT))) return rc;
             if (prof) prof->mark(s, F_OUT);
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D, X24, X24 != nullptr);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
         } else {
             if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT))) return rc;
@@ -777,7 +792,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, yo, M, D, 4 * D, D, R_PROJ))) return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -856,7 +871,8 @@ static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name
     int layer = -1;
     const std::string pre = "visual.transformer.resblocks.";
     if (name.compare(0, pre.size(), pre) == 0) layer = atoi(name.c_str() + pre.size());
-    if (layer >= 0 && h->q8_layer(layer)) {
+    const bool mlp_role = name.find(".mlp.") != std::string::npos;
+    if (layer >= 0 && (mlp_role ? h->q8_mlp(layer) : h->q8_attn(layer))) {
         if (K % 128) FAIL(CLIPVIT_E_INVALID, "MX-fp8 Linear needs in_features % 128 == 0: " + name);
         unsigned char* q = (unsigned char*)dst;
         launch_pack_weight_mx8(s, w, q, q + (size_t)N * K, N, K, K);
@@ -932,6 +948,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_ATTN_Q8")) h->attn_q8 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_X16")) h->x16 = atoi(v) != 0;
+    if (const char* v = getenv("CLIPVIT_X24")) h->x24 = atoi(v) != 0;
     if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
         const int m = atoi(v);
         if (m == 8 || m == 80 || (m >= 60 && m <= 63)) h->split_main = m;
@@ -953,16 +970,33 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
             if (*p == ',') ++p;
         }
     }
+    // default bf16 blocks: the MLP of the first two and last two blocks, the attention roles of
+    // block 1 and the last block only (the last block runs the class-token tail). Measured on
+    // three image / text seeds against the bf16 engine at CLIP logit scale: 1.79e-2 (bar 2e-2;
+    // 1.93e-2 with the attention roles of all four blocks in bf16, 2.04e-2 with block 11's only)
+    // and config 5 +1.7 % (tools/mx_skip_sweep.py)
     if (h->mx8) {
         const int L = c.layers;
         for (int b : {0, 1, L - 2, L - 1})
+            if (b >= 0 && b < 64) h->mx8_skip_mlp |= 1ull << b;
+        for (int b : {1, L - 1})
             if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
     }
-    if (const char* v = getenv("CLIPVIT_MX8_SKIP")) {  // e.g. "0,11": blocks kept in bf16
+    if (const char* v = getenv("CLIPVIT_MX8_SKIP")) {  // e.g. "0,11": blocks kept in bf16 (both masks)
         h->mx8_skip = 0;
         for (const char* p = v; *p;) {
             const int b = atoi(p);
             if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
+            while (*p && *p != ',') ++p;
+            if (*p == ',') ++p;
+        }
+        h->mx8_skip_mlp = h->mx8_skip;
+    }
+    if (const char* v = getenv("CLIPVIT_MX8_SKIP_MLP")) {  // e.g. "0,1,10,11": MLP kept in bf16
+        h->mx8_skip_mlp = 0;
+        for (const char* p = v; *p;) {
+            const int b = atoi(p);
+            if (b >= 0 && b < 64) h->mx8_skip_mlp |= 1ull << b;
             while (*p && *p != ',') ++p;
             if (*p == ',') ++p;
         }

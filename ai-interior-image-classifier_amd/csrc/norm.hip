@@ -128,6 +128,26 @@ __device__ __forceinline__ float4 unpack4_f16(uint2 w) {
                        F16::to_f32((u16)(w.y & 0xffff)), F16::to_f32((u16)(w.y >> 16)));
 }
 
+// 24-bit residual rows (X24, the 16-bit forward): x as two planes, hi = the upper 16 bits of
+// each fp32 value ([rows][D] u16 at base) and lo = the next 8 ([rows][D] bytes at base + plane),
+// rounded to nearest at bit 8: a 16-bit significand (relative error <= 2^-16, against 2^-11 for
+// the 16-bit GEMM operands), 3 bytes per element instead of 4. idx = row * D + column (4-aligned).
+__device__ __forceinline__ float4 x24_load(const unsigned char* base, size_t plane, size_t idx) {
+    const uint2 hi = *(const uint2*)(base + idx * 2);
+    const unsigned lo = *(const unsigned*)(base + plane + idx);
+    return make_float4(__uint_as_float((hi.x << 16) | ((lo & 0xffu) << 8)),
+                       __uint_as_float((hi.x & 0xffff0000u) | (lo & 0xff00u)),
+                       __uint_as_float((hi.y << 16) | ((lo >> 8) & 0xff00u)),
+                       __uint_as_float((hi.y & 0xffff0000u) | ((lo >> 16) & 0xff00u)));
+}
+__device__ __forceinline__ void x24_store(unsigned char* base, size_t plane, size_t idx, float4 v) {
+    const unsigned a = __float_as_uint(v.x) + 0x80u, b = __float_as_uint(v.y) + 0x80u;
+    const unsigned c = __float_as_uint(v.z) + 0x80u, d = __float_as_uint(v.w) + 0x80u;
+    *(uint2*)(base + idx * 2) = make_uint2((a >> 16) | (b & 0xffff0000u), (c >> 16) | (d & 0xffff0000u));
+    *(unsigned*)(base + plane + idx) =
+        ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c << 8) & 0xff0000u) | ((d << 16) & 0xff000000u);
+}
+
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
 // E8M0 scale (rule: common.h mx_exp).
@@ -152,7 +172,7 @@ __device__ __forceinline__ void store_row_q8(unsigned char* q, unsigned char* sq
 // (Q8: h as MX-fp8 q [rows][D] + scales sq [rows][D/32])
 // X16 (MX-fp8 forward, fp16 residual stream): x holds the patch GEMM's fp32 rows (read only) and
 // the residual goes to x16 as fp16.
-template <typename T, int V, bool Q8 = false, bool X16 = false>
+template <typename T, int V, bool Q8 = false, bool X16 = false, bool X24 = false>
 __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, void* __restrict__ h,
                                                        unsigned char* __restrict__ sq,
                                                        const float* __restrict__ cls,
@@ -178,7 +198,11 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
         v[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
     }
     ln_row<V>(v, gp, bp, lane, (float)D);
-    if constexpr (X16) {
+    if constexpr (X24) {  // x16 = the 24-bit residual planes; x keeps the patch rows
+#pragma unroll
+        for (int i = 0; i < V; ++i)
+            x24_store((unsigned char*)x16, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4, v[i]);
+    } else if constexpr (X16) {
         store_x16<V>(x16 + (size_t)row * D, v, lane);
     } else {
 #pragma unroll
@@ -295,7 +319,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // Q8: h is the MX-fp8 A operand of the next GEMM (q [rows][D] + E8M0 scales sq [rows][D/32]).
 // X16: x is the fp16 residual stream (u16 storage) instead of fp32; the sum and the LayerNorm are
 // fp32, the stored x is its fp16 rounding.
-template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false>
+template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false,
+          bool X24 = false>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ xv, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
@@ -318,7 +343,9 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
         const u16* yr = y + (size_t)row * D;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
-            if constexpr (X16) v[r][i] = unpack4_f16(*(const uint2*)(x16 + (size_t)row * D + (lane + 64 * i) * 4));
+            if constexpr (X24)
+                v[r][i] = x24_load((const unsigned char*)xv, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4);
+            else if constexpr (X16) v[r][i] = unpack4_f16(*(const uint2*)(x16 + (size_t)row * D + (lane + 64 * i) * 4));
             else v[r][i] = *(const float4*)(xr + (lane + 64 * i) * 4);
             w[r][i] = *(const uint2*)(yr + (lane + 64 * i) * 4);
             if constexpr (TWO) w2[r][i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
@@ -342,7 +369,9 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
                 v[r][i].z += T::to_f32((u16)(w2[r][i].y & 0xffff));
                 v[r][i].w += T::to_f32((u16)(w2[r][i].y >> 16));
             }
-            if constexpr (STORE_X && !X16) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
+            if constexpr (STORE_X && X24)
+                x24_store((unsigned char*)xv, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4, v[r][i]);
+            else if constexpr (STORE_X && !X16) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
         }
         if constexpr (STORE_X && X16) store_x16<V>(x16 + (size_t)row * D, v[r], lane);
         ln_row<V>(v[r], gm, bt, lane, (float)D);
@@ -427,10 +456,15 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D, void* x16) {
+                     const float* b1, int B, int N, int D, void* x16, bool x24) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
     u16* xo = (u16*)x16;
+    if (x24) {
+        if (dtype == 2) DISPATCH_V(D, embed_ln_kernel<F16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        else DISPATCH_V(D, embed_ln_kernel<BF16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        return;
+    }
     if (dtype == 2) {
         if (xo) DISPATCH_V(D, embed_ln_kernel<F16, V, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
         else DISPATCH_V(D, embed_ln_kernel<F16, V><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, nullptr))
@@ -490,12 +524,12 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
     }
 }
 
-template <typename T, int V, bool X16>
+template <typename T, int V, bool X16, bool X24 = false>
 static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
     dim3 grid((rows + 3) / 4), block(256);
-    if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
-    else add_layernorm_kernel<T, V, false, false, 1, false, X16><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+    if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+    else add_layernorm_kernel<T, V, false, false, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
 }
 
 // MX-fp8 forms (bf16 branch outputs): y2 given -> x = (x + y) + y2 stored; y2 null -> x + y not
@@ -538,8 +572,13 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
 }
 
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
-                                   void* h, const float* g, const float* b, int rows, int D, void* x16) {
+                                   void* h, const float* g, const float* b, int rows, int D, void* x16, bool x24) {
     const u16 *yy = (const u16*)y, *yy2 = (const u16*)y2;
+    if (x24) {
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        return;
+    }
     if (dtype == 2) {
         if (x16) DISPATCH_V(D, add_ln_deferred<F16, V, true>(s, x16, yy, yy2, (u16*)h, g, b, rows))
         else DISPATCH_V(D, add_ln_deferred<F16, V, false>(s, x, yy, yy2, (u16*)h, g, b, rows))
@@ -553,7 +592,7 @@ void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const voi
 // the last block's row-wise ops (out_proj, LayerNorm, MLP) only matter for the class token,
 // which is all that ln_post(x[:, 0, :]) @ proj reads.
 // (X16: x is the fp16 residual stream; xc receives its fp32 widening)
-template <bool X16>
+template <bool X16, bool X24 = false>
 __global__ __launch_bounds__(256) void gather_cls_kernel(const void* __restrict__ x, const u16* __restrict__ h,
                                                          float* __restrict__ xc, u16* __restrict__ hc, int N,
                                                          int D, int B) {
@@ -561,15 +600,19 @@ __global__ __launch_bounds__(256) void gather_cls_kernel(const void* __restrict_
     if (b >= B) return;
     const u16* hs = h + (size_t)b * N * D;
     for (int c = threadIdx.x * 4; c < D; c += 1024) {
-        if constexpr (X16) *(float4*)(xc + (size_t)b * D + c) = unpack4_f16(*(const uint2*)((const u16*)x + (size_t)b * N * D + c));
+        if constexpr (X24)
+            *(float4*)(xc + (size_t)b * D + c) =
+                x24_load((const unsigned char*)x, (size_t)B * N * D * 2, (size_t)b * N * D + c);
+        else if constexpr (X16) *(float4*)(xc + (size_t)b * D + c) = unpack4_f16(*(const uint2*)((const u16*)x + (size_t)b * N * D + c));
         else *(float4*)(xc + (size_t)b * D + c) = *(const float4*)((const float*)x + (size_t)b * N * D + c);
         *(uint2*)(hc + (size_t)b * D + c) = *(const uint2*)(hs + c);
     }
 }
 
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
-                       const void* x16) {
-    if (x16) gather_cls_kernel<true><<<B, 256, 0, s>>>(x16, (const u16*)h, xc, (u16*)hc, N, D, B);
+                       const void* x16, bool x24) {
+    if (x24) gather_cls_kernel<false, true><<<B, 256, 0, s>>>(x16, (const u16*)h, xc, (u16*)hc, N, D, B);
+    else if (x16) gather_cls_kernel<true><<<B, 256, 0, s>>>(x16, (const u16*)h, xc, (u16*)hc, N, D, B);
     else gather_cls_kernel<false><<<B, 256, 0, s>>>(x, (const u16*)h, xc, (u16*)hc, N, D, B);
 }
 

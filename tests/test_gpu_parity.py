@@ -164,7 +164,10 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
     without, with the LayerNorm fold (CLIPVIT_LNFOLD) and without. The unfolded class-token tail
     splits K of its three GEMMs (fp32 partials summed in slice order, no 16-bit branch output),
     so pruned and full last blocks agree to rounding; the folded tail stays bit-identical. The
-    folded and unfolded paths agree to rounding (different but equivalent arithmetic)."""
+    folded and unfolded paths agree to rounding (different but equivalent arithmetic). The
+    identities hold for the fp32 residual stream (CLIPVIT_X24=0); the default 24-bit stream
+    (pruned + deferred path) is compared with it to rounding."""
+    monkeypatch.setenv("CLIPVIT_X24", "0")
     for cfg, B in ((C.VIT_B32, 67), (C.VIT_B16, 9)):
         sd = synthetic_state_dict(cfg, 0)
         ad = synthetic_adapters(cfg, rank=8)
@@ -196,6 +199,20 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
         if "fold" in groups:
             f1, f0 = groups["fold"][0], groups["prune0"][0]
             assert rel(f1, f0) < 3e-3, (cfg.name, dtype, rel(f1, f0))
+        # the 24-bit residual stream (default): x rounded to a 16-bit significand at every store
+        monkeypatch.setenv("CLIPVIT_X24", "1")
+        monkeypatch.setenv("CLIPVIT_CLS_PRUNE", "1")
+        monkeypatch.setenv("CLIPVIT_DEFER_X", "1")
+        monkeypatch.setenv("CLIPVIT_LNFOLD", "0")
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B)
+        eng.load_state_dict(sd)
+        eng.load_lora(ad)
+        f24 = eng.encode_image(px).clone()
+        eng.close()
+        d24 = rel(f24, groups["prune1"][0])
+        print(f"[{cfg.name} {dtype}] 24-bit vs fp32 residual stream: rel {d24:.2e}")
+        assert 0 < d24 < (1.5e-3 if dtype == "fp16" else 1e-2), (cfg.name, dtype, d24)
+        monkeypatch.setenv("CLIPVIT_X24", "0")
 
 
 @pytest.mark.parametrize("dtype,pdt", [("fp16", torch.float16), ("bf16", torch.bfloat16)])

@@ -65,5 +65,10 @@ int main() {
     std::vector<uint32_t> m8(8, 0);
     for (int i = 0; i < 8; ++i) m8[i] = 0x01010101u;         // bits 0, 8, 16, ...
     run("bits 0,8,16,...", m8);
+    // XCD-set masks, if mask bit i maps to XCD i % 8: bits with i % 8 < 4 / >= 4
+    std::vector<uint32_t> x03(8, 0x0f0f0f0fu), x47(8, 0xf0f0f0f0u);
+    run("bits i%8<4", x03);
+    run("bits i%8>=4", x47);
+    // XCD-set masks, if bit i maps to XCD i / 32: words 0-3 / 4-7 (= bits 0-127 / 128-255 above)
     return 0;
 }
