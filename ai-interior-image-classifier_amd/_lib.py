@@ -26,7 +26,7 @@ EXPORTS = (
     "clipvit_profile_forward", "clipvit_gemm_bench", "clipvit_quant_mx8_test",
     "clipvit_gemm_mx8_test", "clipvit_preprocess", "clipvit_resample_plan",
     "clipvit_text_create", "clipvit_text_load_weights", "clipvit_text_load_lora",
-    "clipvit_encode_text", "clipvit_text_destroy",
+    "clipvit_encode_text", "clipvit_text_destroy", "clipvit_residual_x24_test",
 )
 
 
@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
             "clipvit_abi_version": (i, []),
             "clipvit_gemm_test": (i, [vp, i, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_attention_test": (i, [vp, i, vp, vp, i, i, i, i]),
+            "clipvit_residual_x24_test": (i, [vp, vp, vp, vp, ctypes.c_size_t]),
             "clipvit_quant_mx8_test": (i, [vp, i, vp, i, i, vp, vp]),
             "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),

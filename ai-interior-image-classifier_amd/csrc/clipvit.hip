@@ -1400,6 +1400,14 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     return 0;
 }
 
+int clipvit_residual_x24_test(void* stream, const float* x_dev, void* planes_dev, float* back_dev, size_t n) {
+    g_err.clear();
+    if (!x_dev || !planes_dev || !back_dev || n == 0 || n % 4) FAIL(CLIPVIT_E_INVALID, "bad argument");
+    launch_x24_roundtrip((hipStream_t)stream, x_dev, planes_dev, back_dev, n);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 int clipvit_quant_mx8_test(void* stream, int in_dtype, const void* src_dev, int rows, int K,
                            unsigned char* q_dev, unsigned char* sq_dev) {
     g_err.clear();

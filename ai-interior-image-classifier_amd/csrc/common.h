@@ -317,6 +317,7 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
                                    void* h, const float* g, const float* b, int rows, int D, void* x16 = nullptr,
                                    bool x24 = false);
+void launch_x24_roundtrip(hipStream_t s, const float* x, void* planes, float* back, size_t n);
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
                        const void* x16 = nullptr, bool x24 = false);
 void launch_layernorm_q8(hipStream_t s, const float* x, unsigned char* q, unsigned char* sq,

@@ -609,6 +609,19 @@ __global__ __launch_bounds__(256) void gather_cls_kernel(const void* __restrict_
     }
 }
 
+// x24 round trip (clipvit_residual_x24_test): encode n fp32 values into the planes, decode back
+__global__ void x24_roundtrip_kernel(const float* __restrict__ x, unsigned char* __restrict__ planes,
+                                     float* __restrict__ back, size_t n) {
+    const size_t i = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i >= n) return;
+    x24_store(planes, n * 2, i, *(const float4*)(x + i));
+    *(float4*)(back + i) = x24_load(planes, n * 2, i);
+}
+void launch_x24_roundtrip(hipStream_t s, const float* x, void* planes, float* back, size_t n) {
+    const unsigned g = (unsigned)((n / 4 + 255) / 256);
+    x24_roundtrip_kernel<<<g, 256, 0, s>>>(x, (unsigned char*)planes, back, n);
+}
+
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
                        const void* x16, bool x24) {
     if (x24) gather_cls_kernel<false, true><<<B, 256, 0, s>>>(x16, (const u16*)h, xc, (u16*)hc, N, D, B);

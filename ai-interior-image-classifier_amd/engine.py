@@ -248,6 +248,19 @@ def gemm_mx8_test(A8: torch.Tensor, sA: torch.Tensor, W: torch.Tensor, bias: tor
     return (C, sC) if epi in (3, 4) else C
 
 
+def residual_x24_test(x: torch.Tensor) -> torch.Tensor:
+    """fp32 x (numel % 4 == 0) through the 24-bit residual planes and back (norm.hip x24_store /
+    x24_load)."""
+    L = _lib.lib()
+    x = x.contiguous()
+    planes = torch.empty(x.numel() * 3, dtype=torch.uint8, device=x.device)
+    back = torch.empty_like(x)
+    with torch.cuda.device(x.device):
+        s = ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        _lib.check(L.clipvit_residual_x24_test(s, _vp(x), _vp(planes), _vp(back), x.numel()))
+    return back
+
+
 def attention_test(qkv: torch.Tensor, B: int, N: int, H: int, causal: bool = False) -> torch.Tensor:
     L = _lib.lib()
     out = torch.empty((B * N, H * 64), dtype=qkv.dtype, device=qkv.device)

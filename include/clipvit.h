@@ -245,6 +245,11 @@ int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsig
                           const float* W_dev, const float* bias_dev, void* C_dev,
                           unsigned char* sC_dev, int M, int N, int K, int epi, int variant);
 
+/* The 24-bit residual stream format of the 16-bit forward: x fp32 [n] (n % 4 == 0)
+ * -> planes [3n bytes: n u16 upper halves, then n bytes of the next 8 mantissa bits, rounded to
+ * nearest at bit 8] -> back fp32 [n], by the kernels' own encode / decode functions. */
+int clipvit_residual_x24_test(void* stream, const float* x_dev, void* planes_dev, float* back_dev, size_t n);
+
 /* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
  * out [B*N, H*64] of `dtype`. causal != 0: key j masked for query i < j (the text tower). */
 int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B,

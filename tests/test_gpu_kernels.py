@@ -233,3 +233,28 @@ def test_ping_pong_race_screen(gpu, M, N, K):
             for _ in range(6):
                 C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
+
+
+def test_residual_x24_round_trip(gpu):
+    """The 24-bit residual stream (the 16-bit forward's x between the LayerNorm kernels): the
+    upper 16 bits of each fp32 value plus the next 8, rounded to nearest at bit 8 (a carry into
+    the exponent rounds up to the next binade). The device round trip equals that rule bit for
+    bit and stays within 2^-16 relative."""
+    g = torch.Generator().manual_seed(24)
+    x = torch.cat([torch.randn(4096, generator=g) * 10.0 ** torch.randint(-6, 6, (4096,), generator=g),
+                   torch.tensor([0.0, -0.0, 1.0, -1.0, 2.0 ** -20, 65504.0, 1e30, -3.0e-38]),
+                   # values on and beside the rounding boundary of bit 8
+                   torch.tensor([1.0, 1.0]).view(torch.int32).add(
+                       torch.tensor([0x7F, 0x80], dtype=torch.int32)).view(torch.float32),
+                   torch.tensor([1.0, -1.0]).view(torch.int32).add(
+                       torch.tensor([0xFFFF80, 0xFFFF7F], dtype=torch.int32)).view(torch.float32)])
+    assert torch.isfinite(x).all()
+    x = x[: x.numel() // 4 * 4]
+    back = E.residual_x24_test(x.to(gpu)).cpu()
+    bits = x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    ref = (((bits + 0x80) & 0xFFFFFF00) & 0xFFFFFFFF).to(torch.int64)
+    ref = torch.where(ref >= 2 ** 31, ref - 2 ** 32, ref).to(torch.int32).view(torch.float32)
+    assert torch.equal(back.view(torch.int32), ref.view(torch.int32))
+    nz = x != 0
+    rel = ((back - x).abs()[nz] / x.abs()[nz]).max().item()
+    assert rel <= 2.0 ** -16, rel
