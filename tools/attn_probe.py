@@ -1,7 +1,8 @@
-"""Attention at N = 50 (ViT-B/32): kernel time against batch size and against a plain device
-copy of the same bytes, to see whether the kernel is bandwidth- or latency-bound.
+"""Attention kernel timing. Default: N = 50 (ViT-B/32) against batch size and against a plain
+device copy of the same bytes (bandwidth- or latency-bound?). With arguments "B,N,H" ...: those
+shapes only (e.g. 64,577,16 for a ViT-L/14@336 lane, 128,197,12 for ViT-B/16).
 
-    python tools/attn_probe.py
+    python tools/attn_probe.py [B,N,H ...]
 """
 import sys
 from pathlib import Path
@@ -29,6 +30,13 @@ def timeit(fn, iters=50):
 
 
 dev = torch.device("cuda", 0)
+if len(sys.argv) > 1:
+    for arg in sys.argv[1:]:
+        B, N, H = map(int, arg.split(","))
+        qkv = torch.randn(B * N, 3 * H * 64, device=dev).half()
+        t = timeit(lambda: E.attention_test(qkv, B, N, H), iters=20)
+        print(f"B={B} N={N} H={H}: attention {t:8.1f} us, {4 * B * H * N * N * 64 / t / 1e6:7.1f} TFLOP/s", flush=True)
+    sys.exit(0)
 H, N = 12, 50
 for B in (32, 64, 128, 256, 512):
     qkv = torch.randn(B * N, 3 * H * 64, device=dev).half()
