@@ -18,7 +18,7 @@ for src in "$ROOT"/ai-interior-image-classifier_amd/csrc/*.hip; do
   objs="$objs $o"
 done
 wait
-$HIPCC --offload-arch=gfx950 -shared -fsanitize=address -fsanitize=undefined -o "$OUT/libclipvit_asan.so" $objs
+$HIPCC --offload-arch=gfx950 -shared -fno-gpu-sanitize -fsanitize=address -fsanitize=undefined -o "$OUT/libclipvit_asan.so" $objs
 $HIPCC $FLAGS $SAN -x hip "$ROOT/tools/asan/abi_stress.cpp" -o "$OUT/abi_stress" \
-  -L"$OUT" -lclipvit_asan -Wl,-rpath,"\$ORIGIN" -fsanitize=address -fsanitize=undefined
+  -L"$OUT" -lclipvit_asan -Wl,-rpath,"\$ORIGIN" -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined
 echo "built $OUT/abi_stress"
