@@ -146,9 +146,10 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
     constexpr int LA = (A_BYTES + NT * 16 - 1) / (NT * 16), LW = (W_BYTES + NT * 16 - 1) / (NT * 16);
     static_assert(A_BYTES % 1024 == 0 && W_BYTES % 1024 == 0, "whole-wave staging pieces");
     constexpr int SC_ROWS = BM + BN;                      // one scale dword per row per k-step
-    // every wave issues one 4-byte scale glds per k-step (branch-free); waves past the last
-    // scale row fill a pad area
-    constexpr int STAGE = A_BYTES + W_BYTES + (NT > SC_ROWS ? NT : SC_ROWS) * 4;
+    // every wave issues SCW 4-byte scale glds per k-step (branch-free; SCW = 2 when the tile has
+    // more rows than threads, e.g. 160x128 on 4 waves); lanes past the last scale row fill a pad
+    constexpr int SCW = (SC_ROWS + NT - 1) / NT;
+    constexpr int STAGE = A_BYTES + W_BYTES + SCW * NT * 4;
     static_assert(LA * NT * 16 == A_BYTES && LW * NT * 16 == W_BYTES, "whole staging rounds");
     // one LDS object per ring stage: with the stage index a compile-time constant at every
     // use, alias analysis separates the stage being refilled by LDS-DMA from the one being
@@ -182,11 +183,16 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
         const int row = p >> 7, c = ((p >> 4) & 7) ^ mx_sw(row & 15);
         wsrc[r] = (unsigned)((size_t)(n0 + row) * ldb + c * 16);
     }
-    // scale rows: thread t loads row t's dword (A rows first, then W rows; t >= SC_ROWS: pad)
-    static_assert(SC_ROWS <= NT, "one scale dword per thread");
-    const unsigned char* ssrc = tid < BM ? a.sA + (size_t)min(m0 + tid, mlast) * lds_
-                              : tid < SC_ROWS ? a.sW + (size_t)(n0 + tid - BM) * lds_
-                                              : a.sW + (size_t)n0 * lds_;
+    // scale rows: thread t loads the dwords of rows t (and t + NT when SCW = 2; A rows first,
+    // then W rows; rows >= SC_ROWS: pad)
+    static_assert(SCW <= 2, "at most two scale dwords per thread");
+    auto scale_row = [&](int r) -> const unsigned char* {
+        return r < BM ? a.sA + (size_t)min(m0 + r, mlast) * lds_
+             : r < SC_ROWS ? a.sW + (size_t)(n0 + r - BM) * lds_
+                           : a.sW + (size_t)n0 * lds_;
+    };
+    const unsigned char* ssrc = scale_row(tid);
+    const unsigned char* ssrc2 = scale_row(tid + NT);
 
     // operand staging by buffer loads: constant 32-bit per-lane offsets, k offset in an SGPR
     // (same scheme as gemm_pipe_kernel)
@@ -203,6 +209,9 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
         for (int r = 0; r < LW; ++r) blds16(rsW, wsrc[r], kofs, sW + r * NT * 16 + wave * 1024);
         __builtin_amdgcn_global_load_lds((const GLB_AS void*)(ssrc + kt * 4),
                                          (LDS_AS void*)(sS + wave * 256), 4, 0, 0);
+        if constexpr (SCW == 2)
+            __builtin_amdgcn_global_load_lds((const GLB_AS void*)(ssrc2 + kt * 4),
+                                             (LDS_AS void*)(sS + NT * 4 + wave * 256), 4, 0, 0);
     };
 
     const int lrow = lane & 15, lg = lane >> 4;
@@ -729,7 +738,8 @@ static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persist
 }
 
 // variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves), 3 ping-pong 256x256
-// persistent, 4 ping-pong 256x256 one tile per workgroup
+// persistent, 4 ping-pong 256x256 one tile per workgroup, 5 160x128 (2x2 waves; two per CU,
+// 480 tiles = one round at M = 12,800, N = 768)
 template <typename TO>
 static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
     if (variant == 0) variant = a.N % 256 == 0 ? 1 : 2;
@@ -738,6 +748,7 @@ static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) 
         case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
         case 3: return launch_mx8_pp<TO>(s, epi, a, true);
         case 4: return launch_mx8_pp<TO>(s, epi, a, false);
+        case 5: return launch_mx8_tile<TO, 160, 128, 2, 2>(s, epi, a);
     }
     return -1;
 }
