@@ -177,8 +177,10 @@ struct clipvit_handle {
     // MX-fp8 GEMM tile per role (qkv, out, fc, proj); CLIPVIT_MX8_VARIANTS. 128x128 everywhere:
     // measured at M = 25,600 (bs 512) qkv 88 -> 80 us, c_fc 110 -> 103 us against 128x256
     // out_proj on 160x128 (5): 480 tiles = one round at two per CU where 128x128 needs 1.17
-    // (M = 12,800: 18.2 -> 15.1 us standalone, config 5 +1.7-2.3 % same box)
-    int var8[4] = {3, 5, 2, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
+    // (M = 12,800: 18.2 -> 15.1 us standalone, config 5 +1.7-2.3 % same box). c_fc on the
+    // persistent ping-pong: 51.3 -> 55.8 us standalone, yet config 5 +1.5 % on two boxes (under
+    // the two-lane split a kernel is priced by the CU time it holds)
+    int var8[4] = {3, 5, 3, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
     // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
