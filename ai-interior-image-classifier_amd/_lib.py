@@ -26,7 +26,7 @@ EXPORTS = (
     "clipvit_profile_forward", "clipvit_gemm_bench", "clipvit_quant_mx8_test",
     "clipvit_gemm_mx8_test", "clipvit_preprocess", "clipvit_resample_plan",
     "clipvit_text_create", "clipvit_text_load_weights", "clipvit_text_load_lora",
-    "clipvit_encode_text", "clipvit_text_destroy", "clipvit_residual_x24_test",
+    "clipvit_encode_text", "clipvit_text_destroy", "clipvit_residual_x24_test", "clipvit_set_tuning",
 )
 
 
@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
         vp, i, p_f = ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_float)
         sig = {
             "clipvit_create": (i, [ctypes.POINTER(Config), i, ctypes.POINTER(vp)]),
+            "clipvit_set_tuning": (i, [vp, ctypes.c_char_p]),
             "clipvit_load_weights": (i, [vp, ctypes.POINTER(Tensor), ctypes.c_size_t]),
             "clipvit_load_lora": (i, [vp, ctypes.POINTER(Lora), ctypes.c_size_t]),
             "clipvit_set_text_features": (i, [vp, p_f, i, i, ctypes.POINTER(ctypes.c_int), i]),

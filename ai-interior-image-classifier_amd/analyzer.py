@@ -45,22 +45,44 @@ def synthetic_text_features(texts: list[str], dim: int) -> np.ndarray:
     return out
 
 
+SYNTHETIC = "synthetic"  # explicit opt-in to seeded stand-in weights / text rows (tests, bench)
+
+
 class InteriorAnalyzer:
-    def __init__(self, model: str | ViTConfig = "ViT-B/16", state_dict: dict | None = None,
+    """``state_dict``: the vision tower's weights (OpenAI names), or ``"synthetic"`` for seeded
+    stand-in weights (``weights_seed``). Text rows: ``text_features`` (array or per-segment
+    dict), or ``text_state_dict`` (+ BPE) for the GPU text tower, or ``text_features=
+    "synthetic"`` for crc32-seeded stand-in rows. Like ``clip.load`` in the reference
+    (main.py:152, 241), which never hands back a random model, anything else raises: a silent
+    random model would produce meaningless labels with no error."""
+
+    def __init__(self, model: str | ViTConfig = "ViT-B/16", state_dict: dict | str | None = None,
                  use_lora: bool = False, lora_weights_path: str | None = None, lora_rank: int = 4,
                  lora_alpha: float = 8, device: int | str = 0, compute_dtype: str = "fp16",
                  dataset_json: str | Path = "interior_dataset.json",
-                 text_features: dict[str, np.ndarray] | np.ndarray | None = None,
+                 text_features: dict[str, np.ndarray] | np.ndarray | str | None = None,
                  categories: dict[str, list[str]] | None = None, max_batch: int = 64,
                  weights_seed: int = 0, gpu_preprocess: bool = True,
                  text_state_dict: dict | None = None, bpe_path: str | None = None, tokenizer=None,
                  extra_segments: dict[str, tuple[list[str], list[str]]] | None = None):
         self.gpu_preprocess = bool(gpu_preprocess)  # _transform on the GPU (bit-identical)
         self.cfg = model if isinstance(model, ViTConfig) else get_config(model)
+        if state_dict is None:
+            raise ValueError("InteriorAnalyzer needs vision weights: state_dict=<OpenAI-named state dict> "
+                             "(weights.load_openai_checkpoint reads a local ViT-*.pt), or "
+                             "state_dict='synthetic' for seeded stand-in weights")
+        if isinstance(state_dict, str) and state_dict != SYNTHETIC:
+            raise ValueError(f"state_dict must be a dict or {SYNTHETIC!r}, got {state_dict!r}")
+        if text_features is None and text_state_dict is None:
+            raise ValueError("InteriorAnalyzer needs label features: text_features=<[C, E] rows or "
+                             "{segment: rows}>, text_state_dict=<text tower weights> (+ bpe_path / "
+                             "tokenizer), or text_features='synthetic' for seeded stand-in rows")
+        if isinstance(text_features, str) and text_features != SYNTHETIC:
+            raise ValueError(f"text_features must be an array, a dict or {SYNTHETIC!r}, got {text_features!r}")
         self.engine = VisionEngine(self.cfg, device=device, compute_dtype=compute_dtype,
                                    max_batch=max_batch)
-        self.engine.load_state_dict(state_dict if state_dict is not None
-                                    else synthetic_state_dict(self.cfg, weights_seed))
+        self.engine.load_state_dict(synthetic_state_dict(self.cfg, weights_seed)
+                                    if isinstance(state_dict, str) else state_dict)
         self.use_lora = bool(use_lora)
         self.lora_report = None
         ckpt = None
@@ -79,7 +101,7 @@ class InteriorAnalyzer:
             self.table.segments.append(name)
             self.table.labels.append(list(labels))
             self.table.texts.append(list(texts))
-        if text_features is None and text_state_dict is not None:
+        if text_features is None:
             text_features = self._encode_labels(text_state_dict, ckpt, lora_rank, lora_alpha,
                                                 bpe_path, tokenizer, compute_dtype, device)
         T = self._text_matrix(text_features)
@@ -111,7 +133,7 @@ class InteriorAnalyzer:
 
     def _text_matrix(self, text_features) -> np.ndarray:
         E = self.cfg.embed_dim
-        if text_features is None:
+        if isinstance(text_features, str):  # SYNTHETIC (checked in __init__)
             return synthetic_text_features(self.table.all_texts, E)
         if isinstance(text_features, np.ndarray) or torch.is_tensor(text_features):
             T = np.asarray(text_features, dtype=np.float32)

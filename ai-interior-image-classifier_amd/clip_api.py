@@ -115,26 +115,33 @@ def load(name: str = "ViT-B/16", device: str | int | torch.device = "cuda", jit:
          weights: str | dict | None = None, compute_dtype: str = "fp16", max_batch: int = 64,
          seed: int = 0, text_seed: int = 1, bpe_path=None, text: bool = True):
     """(model, preprocess) like clip.load. ``weights``: a LOCAL OpenAI ``ViT-*.pt`` path (read
-    without executing code from it), a state dict with OpenAI names, or None for seeded
-    synthetic weights (no network here). ``jit`` is accepted and ignored. ``text=False`` skips
-    the text tower."""
+    without executing code from it), a state dict with OpenAI names, or ``"synthetic"`` for
+    seeded stand-in weights (tests, bench). There is no download here, and the reference's
+    ``clip.load`` never returns a random model (main.py:152, 241), so ``weights=None`` raises.
+    ``jit`` is accepted and ignored. ``text=False`` skips the text tower."""
     del jit
+    if weights is None:
+        raise ValueError(f"clip_api.load({name!r}) needs weights: a local OpenAI ViT-*.pt path or a "
+                         "state dict (nothing is downloaded here); weights='synthetic' gives seeded "
+                         "stand-in weights")
+    if not isinstance(weights, (str, os.PathLike, dict)):
+        raise TypeError(f"weights must be a path, a state dict or 'synthetic', got {type(weights).__name__}")
     if bpe_path is not None:
         set_bpe_path(bpe_path)
     cfg = get_config(name)
     dev = torch.device(device if not isinstance(device, int) else f"cuda:{device}")
     if dev.type == "cuda" and dev.index is None:
         dev = torch.device("cuda", torch.cuda.current_device())
-    if isinstance(weights, (str, os.PathLike)):
-        vis_sd = load_openai_checkpoint(weights)
-        txt_sd = load_openai_checkpoint(weights, text=True) if text else None
-    elif isinstance(weights, dict):
-        vis_sd = weights
-        txt_sd = weights if text else None
-    else:
+    if isinstance(weights, str) and weights == "synthetic":
         vis_sd = synthetic_state_dict(cfg, seed)
         vocab = _TOKENIZER.vocab_size if _TOKENIZER is not None else TextConfig().vocab
         txt_sd = synthetic_text_state_dict(text_config_for(cfg, vocab), text_seed) if text else None
+    elif isinstance(weights, (str, os.PathLike)):
+        vis_sd = load_openai_checkpoint(weights)
+        txt_sd = load_openai_checkpoint(weights, text=True) if text else None
+    else:  # dict
+        vis_sd = weights
+        txt_sd = weights if text else None
     if any(n not in vis_sd for n, _ in visual_names(cfg)):
         raise KeyError(f"weights lack the {name} vision tower")
     eng = VisionEngine(cfg, device=dev, compute_dtype=compute_dtype, max_batch=max_batch)

@@ -573,21 +573,10 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
     }
 }
 
-static int attn_v3() {  // CLIPVIT_ATTN_V3: 0 off, 1 (default) long sequences, 2 also N <= 64
-    static const int on = [] {
-        const char* v = getenv("CLIPVIT_ATTN_V3");
-        return v ? atoi(v) : 1;
-    }();
-    return on;
-}
-
-static bool attn_v2() {
-    static const bool on = [] {
-        const char* v = getenv("CLIPVIT_ATTN_V2");
-        return !v || atoi(v) != 0;
-    }();
-    return on;
-}
+// kernel choice by sequence length: attention_v3 (two query fragments per wave) for N > 128,
+// attention_v2 (one key block, ViT-B/32's N = 50) for N <= 64
+static constexpr int attn_v3() { return 1; }  // 1: long sequences only (2 = also N <= 64, measured slower)
+static constexpr bool attn_v2() { return true; }
 
 // attention with the output quantized to MX-fp8 (q8 [B N, D] e4m3 + q8s [B N, D / 32] scales) in
 // the kernel, for the shapes that run on the one-key-block attention_v2 (N <= 64: ViT-B/32);

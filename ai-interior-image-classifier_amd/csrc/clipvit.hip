@@ -400,6 +400,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.lnf_s = fo.s; a.st_in = fo.st_in; a.st_out = fo.st_out; a.C2 = fo.C2; a.np = fo.np;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
+    a.ncu = h->ncu;
     int variant = h->var[role];
     // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
     // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
@@ -417,9 +418,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the main launch's tile width: every pipelined variant a round split can use is 256 wide
     // (8 / 80: 256x256, 98: 240x256)
     const int bn = 256;
+    // (the ping-pong main tiles, split_main >= 60, have the 16-bit STORE / GELU epilogues only:
+    // the LayerNorm-fold epilogues take the single-launch path below)
+    const bool split_epi = epi == EPI_STORE || epi == EPI_GELU ||
+                           ((epi == EPI_LNF || epi == EPI_LNF_GELU) && h->split_main < 60);
     if (h->round_split && !h->var_forced && (role == R_FC || role == R_QKV) && t256 &&
-        N % bn == 0 && t256 < 4L * h->ncu &&
-        (epi == EPI_STORE || epi == EPI_GELU || epi == EPI_LNF || epi == EPI_LNF_GELU)) {
+        N % bn == 0 && t256 < 4L * h->ncu && split_epi) {
         const long nN = N / bn, tm = (long)((M + 255) / 256) * nN;
         const long R = tm / h->ncu, rem = tm % h->ncu;
         const long m1 = R * h->ncu / nN * 256;
@@ -498,6 +502,7 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.bias = bias; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     if (epi == EPI_GELU_Q8) a.sC = (unsigned char*)C + (size_t)M * N;
     a.xcd_n = h->xcd[role];
+    a.ncu = h->ncu;
     const int v8 = h->var8[role];
     if ((v8 == 3 || v8 == 4) && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
     if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, v8) != 0 &&
@@ -941,39 +946,10 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     // 16-bit residual branch outputs for both 16-bit types (bf16 too since r02: measured 76.3k ->
     // 78.9k img/s at bs 256 with the logit error unchanged, 4.35e-3 -> 4.13e-3)
     h->resid16 = true;  // fp16, bf16 and MX-fp8 (its bf16 branch outputs)
-    if (const char* v = getenv("CLIPVIT_RESID16")) h->resid16 = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_DEFER_X")) h->defer_x = atoi(v) != 0;
     // off by default: measured slower (the residual epilogues run in lockstep
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
-    h->lnfold = false;  // <= 8 statistics groups per row (gemm.hip) when enabled
-    if (const char* v = getenv("CLIPVIT_LNFOLD"))
-        h->lnfold = h->resid16 && h->dt == CLIPVIT_F16 && h->D <= 1024 && atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_CLS_PRUNE")) h->cls_prune = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_GEMM_SPLIT")) h->round_split = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_ATTN_Q8")) h->attn_q8 = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_X16")) h->x16 = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_X24")) h->x24 = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_SPLIT_VARIANTS")) {  // main launch: a 256x256 tile (8 or 80)
-        const int m = atoi(v);
-        if (m == 8 || m == 80 || (m >= 60 && m <= 63)) h->split_main = m;
-        if (const char* c = strchr(v, ',')) h->split_tail = atoi(c + 1);
-    }
-    if (const char* v = getenv("CLIPVIT_TAIL_VARIANT")) h->tail_var = atoi(v);
-    if (const char* v = getenv("CLIPVIT_SPLIT_XCD")) h->split_xcd = atoi(v);
-    if (const char* v = getenv("CLIPVIT_MAX_INFLIGHT")) h->max_inflight = std::max(1, atoi(v));
+    h->lnfold = false;
     h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);
-    if (const char* v = getenv("CLIPVIT_SPLIT_MIN")) {
-        h->split_min = atoi(v);
-        if (h->split_min <= 0) h->split_min = SPLIT_NEVER;
-    }
-    if (const char* v = getenv("CLIPVIT_GEMM_XCD")) {
-        int k = 0;
-        for (const char* p = v; *p && k < 5; ++k) {
-            h->xcd[k] = atoi(p);
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-    }
     // default bf16 blocks: the MLP of the first two and last two blocks, the attention roles of
     // block 1 and the last block only (the last block runs the class-token tail). Measured on
     // three image / text seeds against the bf16 engine at CLIP logit scale: 1.79e-2 (bar 2e-2;
@@ -986,56 +962,149 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
         for (int b : {1, L - 1})
             if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
     }
-    if (const char* v = getenv("CLIPVIT_MX8_SKIP")) {  // e.g. "0,11": blocks kept in bf16 (both masks)
-        h->mx8_skip = 0;
-        for (const char* p = v; *p;) {
-            const int b = atoi(p);
-            if (b >= 0 && b < 64) h->mx8_skip |= 1ull << b;
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-        h->mx8_skip_mlp = h->mx8_skip;
-    }
-    if (const char* v = getenv("CLIPVIT_MX8_SKIP_MLP")) {  // e.g. "0,1,10,11": MLP kept in bf16
-        h->mx8_skip_mlp = 0;
-        for (const char* p = v; *p;) {
-            const int b = atoi(p);
-            if (b >= 0 && b < 64) h->mx8_skip_mlp |= 1ull << b;
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-    }
-    if (const char* v = getenv("CLIPVIT_MX8_VARIANTS")) {
-        int k = 0;
-        for (const char* p = v; *p && k < 4; ++k) {
-            h->var8[k] = atoi(p);
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-    }
     {
         int ncu = 0;
         if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
             h->ncu = ncu;
     }
-    if (const char* v = getenv("CLIPVIT_LARGE_VARIANTS")) {  // "q,f[,o,p]"
-        int k = 0;
-        for (const char* p = v; *p && k < 4; ++k) {
-            h->large_var[k] = atoi(p);
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-    }
-    if (const char* v = getenv("CLIPVIT_GEMM_VARIANTS")) {
-        h->var_forced = true;
-        int k = 0;
-        for (const char* p = v; *p && k < 5; ++k) {
-            h->var[k] = atoi(p);
-            while (*p && *p != ',') ++p;
-            if (*p == ',') ++p;
-        }
-    }
     *out = h;
+    return 0;
+}
+
+// ---- clipvit_set_tuning: the measured alternatives of DESIGN.md, for tests and A/B tools only ----
+static bool parse_int(const std::string& v, int& out) {
+    char* e = nullptr;
+    const long x = strtol(v.c_str(), &e, 10);
+    if (v.empty() || !e || *e) return false;
+    out = (int)x;
+    return true;
+}
+// "a,b,c" -> up to n ints; every field must parse
+static bool parse_list(const std::string& v, int* out, int n) {
+    size_t pos = 0;
+    for (int k = 0; k < n && pos <= v.size(); ++k) {
+        const size_t q = v.find(',', pos);
+        if (!parse_int(v.substr(pos, q == std::string::npos ? std::string::npos : q - pos), out[k])) return false;
+        if (q == std::string::npos) return true;
+        pos = q + 1;
+    }
+    return pos > v.size();
+}
+// "i,j,..." -> bit mask of block indices ("" = none)
+static bool parse_mask(const std::string& v, uint64_t& m) {
+    m = 0;
+    size_t pos = 0;
+    while (pos < v.size()) {
+        const size_t q = v.find(',', pos);
+        int b = 0;
+        if (!parse_int(v.substr(pos, q == std::string::npos ? std::string::npos : q - pos), b) || b < 0 || b >= 64)
+            return false;
+        m |= 1ull << b;
+        if (q == std::string::npos) break;
+        pos = q + 1;
+    }
+    return true;
+}
+
+static int apply_tuning(clipvit_handle* h, const std::string& k, const std::string& v) {
+    int x = 0;
+    auto flag = [&](bool& dst) {
+        if (!parse_int(v, x)) return false;
+        dst = x != 0;
+        return true;
+    };
+    bool ok = true;
+    if (k == "resid16") ok = flag(h->resid16);
+    else if (k == "defer_x") ok = flag(h->defer_x);
+    else if (k == "lnfold") {  // fp16 only, D <= 1024 (<= 8 statistics groups per row)
+        bool f = false;
+        ok = flag(f);
+        h->lnfold = f && h->resid16 && h->dt == CLIPVIT_F16 && h->D <= 1024;
+    } else if (k == "cls_prune") ok = flag(h->cls_prune);
+    else if (k == "round_split") ok = flag(h->round_split);
+    else if (k == "attn_q8") ok = flag(h->attn_q8);
+    else if (k == "x16") ok = flag(h->x16);
+    else if (k == "x24") ok = flag(h->x24);
+    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62-64)
+        int m[2] = {h->split_main, h->split_tail};
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || (m[0] >= 62 && m[0] <= 64));
+        if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
+    } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
+    else if (k == "split_xcd") ok = parse_int(v, h->split_xcd);
+    else if (k == "max_inflight") {
+        ok = parse_int(v, x) && x >= 1;
+        if (ok) h->max_inflight = x;
+    } else if (k == "split_min") {  // <= 0: never split
+        ok = parse_int(v, x);
+        if (ok) h->split_min = x <= 0 ? SPLIT_NEVER : x;
+    } else if (k == "gemm_xcd") ok = parse_list(v, h->xcd, 5);
+    else if (k == "mx8_skip") {  // both masks
+        ok = parse_mask(v, h->mx8_skip);
+        if (ok) h->mx8_skip_mlp = h->mx8_skip;
+    } else if (k == "mx8_skip_mlp") ok = parse_mask(v, h->mx8_skip_mlp);
+    else if (k == "mx8_variants") ok = parse_list(v, h->var8, 4);
+    else if (k == "large_variants") ok = parse_list(v, h->large_var, 4);
+    else if (k == "gemm_variants") {
+        ok = parse_list(v, h->var, 5);
+        h->var_forced = ok;
+    } else FAIL(CLIPVIT_E_INVALID, "unknown tuning key '" + k + "'");
+    if (!ok) FAIL(CLIPVIT_E_INVALID, "bad tuning value " + k + "=" + v);
+    return 0;
+}
+
+int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
+    g_err.clear();
+    if (!h || !spec) FAIL(CLIPVIT_E_INVALID, "null argument");
+    if (h->loaded || !h->pool.empty()) FAIL(CLIPVIT_E_STATE, "tuning must precede clipvit_load_weights");
+    const std::string all(spec);
+    struct KV { std::string k, v; };
+    std::vector<KV> kv;
+    size_t pos = 0;
+    while (pos < all.size()) {
+        size_t q = all.find(';', pos);
+        if (q == std::string::npos) q = all.size();
+        const std::string item = all.substr(pos, q - pos);
+        pos = q + 1;
+        if (item.empty()) continue;
+        const size_t eq = item.find('=');
+        if (eq == std::string::npos) FAIL(CLIPVIT_E_INVALID, "tuning item without '=': " + item);
+        kv.push_back({item.substr(0, eq), item.substr(eq + 1)});
+    }
+    // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
+    struct Tun {
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced;
+        int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min;
+        int xcd[5], var8[4], large_var[4], var[5];
+        uint64_t mx8_skip, mx8_skip_mlp;
+    };
+    auto save = [](const clipvit_handle* g) {
+        Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
+              g->var_forced, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
+              g->split_min, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
+        memcpy(t.xcd, g->xcd, sizeof t.xcd);
+        memcpy(t.var8, g->var8, sizeof t.var8);
+        memcpy(t.large_var, g->large_var, sizeof t.large_var);
+        memcpy(t.var, g->var, sizeof t.var);
+        return t;
+    };
+    const Tun before = save(h);
+    for (const auto& e : kv) {
+        const int rc = apply_tuning(h, e.k, e.v);
+        if (rc) {
+            h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
+            h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
+            h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced;
+            h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
+            h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
+            memcpy(h->xcd, before.xcd, sizeof before.xcd);
+            memcpy(h->var8, before.var8, sizeof before.var8);
+            memcpy(h->large_var, before.large_var, sizeof before.large_var);
+            memcpy(h->var, before.var, sizeof before.var);
+            h->mx8_skip = before.mx8_skip;
+            h->mx8_skip_mlp = before.mx8_skip_mlp;
+            return rc;
+        }
+    }
     return 0;
 }
 
@@ -1312,13 +1381,16 @@ int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_
     int cnt[F_COUNT] = {0};
     for (size_t k = 1; k < p.k; ++k) ++cnt[p.fam[k]];
     float gap = 0.f;
-    if (!rc) {
+    if (!rc) {  // events of its own (p.ev holds 8 + 8 L, which a 1-layer model makes < 17)
         constexpr int NG = 17;
-        for (int k = 0; k < NG; ++k) hipEventRecord(p.ev[k], s);
-        hipEventSynchronize(p.ev[NG - 1]);
+        hipEvent_t g[NG];
+        for (auto& e : g) hipEventCreate(&e);
+        for (int k = 0; k < NG; ++k) hipEventRecord(g[k], s);
+        hipEventSynchronize(g[NG - 1]);
         float ms = 0.f;
-        hipEventElapsedTime(&ms, p.ev[0], p.ev[NG - 1]);
+        hipEventElapsedTime(&ms, g[0], g[NG - 1]);
         gap = ms / (NG - 1);
+        for (auto& e : g) hipEventDestroy(e);
     }
     hipEventRecord(l->done, s);
     for (auto& e : p.ev) hipEventDestroy(e);
@@ -1358,6 +1430,14 @@ int clipvit_destroy(clipvit_handle* h) {
 }
 
 // ---- kernel-level test entry points ----
+// compute units of the current device (the persistent GEMMs' grid)
+static int current_ncu() {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
+        return 0;
+    return n;
+}
+
 int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi, int variant) {
     g_err.clear();
@@ -1371,13 +1451,14 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     GemmArgs a{};
     a.A = A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
+    a.ncu = current_ncu();
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 60 ||
-                        variant == 61 || variant == 62 || variant == 63;
+                        variant == 61 || variant == 62 || variant == 63 || variant == 64;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;
@@ -1439,6 +1520,7 @@ int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsig
     a.A = A8_dev; a.sA = sA_dev; a.W = Wq; a.sW = Wq + (size_t)N * K;
     a.bias = bias_dev; a.C = C_dev; a.sC = sC_dev;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
+    a.ncu = current_ncu();
     a.xcd_n = variant / 100;
     static const int emap[6] = {EPI_F32, EPI_F32GELU, EPI_RESID, EPI_Q8, EPI_GELU_Q8, EPI_STORE};
     const int rc = launch_gemm_mx8(s, CLIPVIT_BF16, emap[epi], a, variant % 100);
@@ -1477,7 +1559,9 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.patch_g2 = 49; a.patch_ntok = 50;
     a.xcd_n = variant / 100;
     variant %= 100;
-    if (const char* v = getenv("CLIPVIT_PP_DELAY")) a.pp_delay = atoi(v);  // bench of the stagger
+    a.ncu = current_ncu();
+    // diagnostic: persistent GEMMs on fewer workgroups (store-burst experiments)
+    if (const char* v = getenv("CLIPVIT_BENCH_GRID")) a.ncu = atoi(v);
     int e = epi;  // raw Epi enum
     if (mx) {
         a.sA = (const unsigned char*)A + (size_t)M * K;

@@ -169,10 +169,9 @@ struct GemmArgs {
     // split-K (EPI_F32 on the pipelined tiles only): grid.y = ksplit slices of K / ksplit each;
     // slice z writes its fp32 partial (no bias) to C + z * M * ldc. 0 / 1 = no split
     int ksplit;
-    // persistent ping-pong GEMM (gemm_pp.hip, variant 62): workgroups with fewer tiles than the
-    // busiest ones start pp_delay x 8k cycles x (their rank mod 4) / 4 late, so the epilogue store
-    // bursts of a round do not all fall at once (0 = off)
-    int pp_delay;
+    // compute units of the device the GEMM runs on: the persistent kernels' grid size
+    // (0 = assume 256, MI355X)
+    int ncu;
 };
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,

@@ -285,7 +285,15 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // (bias, QuickGELU, 16-bit stores straight from the accumulators) runs in the first read
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
-template <typename T, int EPI, bool NT = false>
+//
+// RC (variant 64): row-contiguous epilogue stores. From the accumulators a lane holds 32 B of one
+// token row, so a plain store instruction writes 16 B into each of 16 rows per quarter-wave: the
+// CU's store pipe then moves ~16 partial lines per 256 B and one CU's 128 KB tile takes ~3.7 us
+// to leave it even on an idle chip (tools/probes/store_probe.hip: 5.7 us with one tile per CU on
+// 8 CUs, 2.7 us for the same bytes as whole 128-B rows). RC bounces every 16-row slab of the
+// wave (2 KB) through a private LDS slot in the free end of the bias region (N <= 4096) and
+// stores 8 whole rows per instruction.
+template <typename T, int EPI, bool NT = false, bool RC = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -293,6 +301,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     constexpr int NBIAS = 8192;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 160 KB
     float* const colv = (float*)(smem + 2 * STAGE);
+    constexpr int RC_OFF = 2 * STAGE + NBIAS * 4 - 8 * 2048;  // RC slots: bias entries 4096.. (N <= 4096)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -360,13 +369,6 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     for (int i = tid; i < a.N; i += 512) colv[i] = a.bias ? a.bias[i] : 0.f;
     if (grp == 0) vm_wait<2>(); else vm_wait<4>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if (a.pp_delay > 0) {  // fewer tiles than the busiest workgroups: start late (see GemmArgs)
-        const int mine = (ntiles - 1 - (int)blockIdx.x) / G + 1, most = (ntiles - 1) / G + 1;
-        if (mine < most) {
-            const int n = a.pp_delay * (int)((blockIdx.x >> 3) & 3);
-            for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-        }
-    }
     __builtin_amdgcn_s_barrier();
     if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
@@ -495,6 +497,58 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
         }
+        // RC: the wave's LDS slot (2 KB at the end of the LDS image) and its lane addresses:
+        // write row lrow, 16-B chunks 2 lg, 2 lg + 1; read row (lane >> 3) (+ 8), chunk lane & 7;
+        // chunk c of row r sits at c ^ (r & 7) (conflict-free both ways). Software-pipelined:
+        // slab fm's LDS round trip runs under slab fm + 1's epilogue arithmetic. A wave's LDS
+        // instructions execute in order, so the reads see the slab's writes, and the lgkmcnt(0)
+        // before a slab's stores retires its reads before the next slab overwrites the slot.
+        if constexpr (RC) {
+            const unsigned slot = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + RC_OFF) + wave * 2048;
+            const unsigned wa0 = slot + lrow * 128 + (((2 * lg) ^ lsw) << 4);
+            const unsigned wa1 = slot + lrow * 128 + (((2 * lg + 1) ^ lsw) << 4);
+            const unsigned ra = slot + (lane >> 3) * 128 + (((lane & 7) ^ ((lane >> 3) & 7)) << 4);
+            const int rr0 = m0 + grp * 128 + (lane >> 3);
+            const size_t cb = (size_t)(n0 + wc * 64 + 8 * (lane & 7)) * 2;
+            auto put = [&](int fm, const u32x4& o0, const u32x4& o1) {
+                const int mr = rr0 + fm * 16;
+                const size_t off = (size_t)mr * a.ldc * 2 + cb;
+#if CLIPVIT_ABLATE == 3  // diagnostic build only: no epilogue stores (values kept live)
+                if (a.ldc > (1 << 30)) {
+#else
+                {
+#endif
+                    if (mr < a.M) *(u32x4*)(Cb + off) = o0;
+                    if (mr + 8 < a.M) *(u32x4*)(Cb + off + (size_t)8 * a.ldc * 2) = o1;
+                }
+            };
+            u32x4 o0, o1;
+#pragma unroll
+            for (int fm = 0; fm < 8; ++fm) {
+                float v[16];
+#pragma unroll
+                for (int f = 0; f < 4; ++f)
+#pragma unroll
+                    for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
+                if constexpr (GELU) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                }
+                const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+                const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
+                                  pack2<T>(v[14], v[15])};
+                if (fm > 0) {
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    put(fm - 1, o0, o1);
+                }
+                asm volatile("ds_write_b128 %0, %1" ::"v"(wa0), "v"(w0) : "memory");
+                asm volatile("ds_write_b128 %0, %1" ::"v"(wa1), "v"(w1) : "memory");
+                asm volatile("ds_read_b128 %0, %1" : "=v"(o0) : "v"(ra) : "memory");
+                asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(o1) : "v"(ra) : "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            put(7, o0, o1);
+        } else {
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = m0 + grp * 128 + fm * 16 + lrow;
@@ -525,6 +579,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
                 }
             }
         }
+        }
         if (!has_next) break;
         m0 = mn;
         n0 = nn;
@@ -545,18 +600,13 @@ static int launch_pp_t(hipStream_t s, int epi, const GemmArgs& a, int sm) {
     return -1;
 }
 
-template <typename T, bool NT>
+template <typename T, bool NT, bool RC>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
-    static const int ncu = [] {
-        int d = 0, n = 0;
-        (void)hipGetDevice(&d);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
-        return n > 0 ? n : 256;
-    }();
+    const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, RC><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, RC><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
@@ -564,10 +614,11 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
 // 62: persistent (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with non-temporal stores
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
-    if (variant == 62 || variant == 63) {
-        if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-        if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
-        return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
+    if (variant >= 62 && variant <= 64) {
+        if (a.N > (variant == 64 ? 4096 : 8192) || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
+        if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true, false>(s, epi, a) : launch_ppp_t<BF16, true, false>(s, epi, a);
+        if (variant == 64) return dtype == 2 ? launch_ppp_t<F16, false, true>(s, epi, a) : launch_ppp_t<BF16, false, true>(s, epi, a);
+        return dtype == 2 ? launch_ppp_t<F16, false, false>(s, epi, a) : launch_ppp_t<BF16, false, false>(s, epi, a);
     }
     const int sm = variant == 61 ? 3 : 0;
     return dtype == 2 ? launch_pp_t<F16>(s, epi, a, sm) : launch_pp_t<BF16>(s, epi, a, sm);

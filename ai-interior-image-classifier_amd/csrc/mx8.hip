@@ -724,12 +724,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
 template <typename TO>
 static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persistent) {
     if (a.N % 256 || a.K % 256 || a.N > 4096 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-    static const int ncu = [] {
-        int d = 0, n = 0;
-        (void)hipGetDevice(&d);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d);
-        return n > 0 ? n : 256;
-    }();
+    const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = persistent && ntiles > ncu ? ncu : ntiles;
     if (epi == EPI_STORE) { gemm_mx8_pp_kernel<TO, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }

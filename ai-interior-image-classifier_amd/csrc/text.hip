@@ -218,15 +218,6 @@ int clipvit_text_create(const clipvit_text_config* cfg, int device, clipvit_text
     h->device = device;
     h->dt = c.compute_dtype;
     h->resid16 = true;  // both 16-bit types, as the vision tower
-    if (const char* v = getenv("CLIPVIT_TEXT_RESID16")) h->resid16 = atoi(v) != 0;
-    if (const char* v = getenv("CLIPVIT_TEXT_VARIANTS")) {
-        int k = 0;
-        for (const char* q = v; *q && k < 4; ++k) {
-            h->var[k] = atoi(q);
-            while (*q && *q != ',') ++q;
-            if (*q == ',') ++q;
-        }
-    }
     *out = h;
     return 0;
 }

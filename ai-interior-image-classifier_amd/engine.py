@@ -41,7 +41,9 @@ class ClassifyOutput:
 
 class VisionEngine:
     def __init__(self, cfg: ViTConfig, device: int | str | torch.device = 0,
-                 compute_dtype: str = "fp16", max_batch: int = 256):
+                 compute_dtype: str = "fp16", max_batch: int = 256, tuning: dict | str | None = None):
+        """``tuning``: tests and A/B tools only — one of DESIGN.md's measured alternatives
+        instead of the shipped default (clipvit_set_tuning; e.g. ``{"split_min": 0}``)."""
         if not torch.cuda.is_available():
             raise _lib.ClipVitError(_lib.E_STATE, "no HIP device visible: the MI355X path needs a GPU")
         dev = torch.device(device if not isinstance(device, int) else f"cuda:{device}")
@@ -57,6 +59,14 @@ class VisionEngine:
         h = ctypes.c_void_p()
         _lib.check(self._L.clipvit_create(ctypes.byref(c), self.device.index, ctypes.byref(h)))
         self._h = h
+        if tuning:
+            spec = tuning if isinstance(tuning, str) else ";".join(f"{k}={v}" for k, v in tuning.items())
+            try:
+                _lib.check(self._L.clipvit_set_tuning(h, spec.encode()))
+            except Exception:
+                self.close()
+                raise
+        self.tuning = tuning
         self.C = 0
         self.seg_offsets: list[int] = []
         self.loaded = False

@@ -26,8 +26,11 @@
 extern "C" {
 #endif
 
-/* 2: clipvit_attention_test takes `causal` (8 arguments; version 1 had 7). */
-#define CLIPVIT_ABI_VERSION 2
+/* 2: clipvit_attention_test takes `causal` (8 arguments; version 1 had 7), and
+ *    clipvit_profile_forward writes 20 floats to out_ms (version 1 wrote 10: a version-1 caller's
+ *    10-float buffer overflows).
+ * 3: clipvit_set_tuning (the library reads no environment variables). */
+#define CLIPVIT_ABI_VERSION 3
 
 /* Status codes. */
 #define CLIPVIT_OK 0
@@ -89,6 +92,16 @@ typedef struct clipvit_handle clipvit_handle;
 /* Replaces clip.load(name, device) model construction (main.py:152, main.py:241).
  * Allocates the weight store and the first workspace for cfg->max_batch images. */
 int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
+
+/* Test / A-B hook, not part of the reference's surface: select one of the measured
+ * alternatives DESIGN.md records instead of the shipped default, before clipvit_load_weights
+ * (CLIPVIT_E_STATE after it). spec = "key=value;key=value", keys: resid16, defer_x, lnfold,
+ * cls_prune, round_split, attn_q8, x16, x24 (0/1); split_variants "main,tail"; tail_variant;
+ * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
+ * large_variants "q,f,o,p"; mx8_variants "q,o,f,p"; mx8_skip / mx8_skip_mlp "i,j,.." (bf16
+ * blocks; mx8_skip sets both masks). An unknown key or bad value fails with CLIPVIT_E_INVALID
+ * and leaves the handle unchanged. The product path never calls it. */
+int clipvit_set_tuning(clipvit_handle* h, const char* spec);
 
 /* Replaces the weight half of clip.load [3p]: host fp32 tensors keyed by OpenAI names.
  * The library copies them to HBM, keeps fp32 masters, and packs the MFMA operands.

@@ -2,7 +2,10 @@
 two torchrun ranks share cuda:0 (--share-gpu: gloo, since RCCL refuses two ranks on one device).
 Checks the line's contract: the per-rank barrier and max-over-ranks timing ran, the value counts
 both ranks' images, and the rehearsal is labelled as such (n_gpus 1, ranks 2, not a scaling
-point). The RCCL calls themselves are checked by tools/rccl_check.py."""
+point), and the line reports what the collective did: the world size the process group saw, its
+backend, and gather_ok (rank 0's slice of the gathered logits equals its local logits bit for
+bit, checked once after the timed loop). On the driver's N-GPU runs the backend is nccl (RCCL);
+here it is gloo. The RCCL calls themselves are checked by tools/rccl_check.py."""
 import json
 import os
 import subprocess
@@ -31,3 +34,5 @@ def test_bench_two_rank_rehearsal(gpu):
     assert d["config"]["global_batch"] == 64 and d["steps"] == 3
     assert d["value"] > 0 and abs(d["value"] - 64 * 3 / (d["ms_per_step"] * 3e-3)) / d["value"] < 1e-3
     assert d["parity"]["meets_bar"], d["parity"]
+    assert d["rccl_world"] == 2 and d["backend"] == "gloo" and d["gather_ok"] is True, d
+    assert d["gathered_rows"] == 64

@@ -42,6 +42,7 @@ from interior_amd.weights import synthetic_text_state_dict
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
+FLAT_TOL = 3e-3  # flat fixtures: twice the committed worst image (1.42e-3, r03), not the bar
 GAP_TOL = 1e-4   # fixture probability gap below which two labels may swap
 PROB_TOL = 2e-3
 TEXT_TOL = 2e-3
@@ -98,10 +99,12 @@ def _compare(ref, got, where, tie_gap, ref_logits, js, check_reason=True, logit_
     # a softmax moves by at most half the max |dlogit| (|dp_S| <= 2 p_S (1 - p_S) e, any label
     # set S), so the probability bound follows from the measured logit error
     ptol = max(PROB_TOL, 0.55 * logit_err)
+    # labels compared here (detector category + every analysis entry): the swap-count bound's base
+    count = {} if count is None else count
+    count["checked"] = count.get("checked", 0) + 1 + sum(len(v) for v in ref["analysis"].values())
     assert got["is_interior"] == ref["is_interior"], where
     assert abs(got["interior_confidence"] - ref["interior_confidence"]) < ptol, where
-    count = {} if count is None else count
-    n0 = sum(count.values())
+    n0 = count.get("gap", 0) + count.get("err", 0)
 
     def swap(z, a, b, what):
         p = _softmax(z)
@@ -127,7 +130,13 @@ def _compare(ref, got, where, tie_gap, ref_logits, js, check_reason=True, logit_
             assert abs(gp - rp) < ptol, (where, cat, j, gp, rp, ptol)
             if gl != rl:
                 swap(z, labs.index(gl), labs.index(rl), (cat, j))
-    return sum(count.values()) - n0
+    return count.get("gap", 0) + count.get("err", 0) - n0
+
+
+def _swap_bound(cnt, what, frac=0.02):
+    """near-tie label swaps are allowed one by one, so their number is bounded too."""
+    n = cnt.get("gap", 0) + cnt.get("err", 0) + cnt.get("detector", 0)
+    assert n <= frac * max(cnt.get("checked", 0), 1), (what, cnt)
 
 
 @pytest.mark.parametrize("model,ckpt", CASES)
@@ -136,7 +145,7 @@ def test_flat_fixtures_results_match_reference_harness(gpu, golden_dir, images, 
     names, imgs = images
     assert js["images"] == names and js["detector_categories"] == L.DETECTOR_CATEGORIES
     an = InteriorAnalyzer(model=js["model"], device=0, categories=js["categories"], text_features=T,
-                          weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
+                          state_dict="synthetic", weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
                           lora_weights_path=str(golden_dir / "lora" / js["checkpoint"]))
     assert an.engine.compute_dtype == "fp16" and an.lora_report["loaded"] == 48
     try:
@@ -148,7 +157,9 @@ def test_flat_fixtures_results_match_reference_harness(gpu, golden_dir, images, 
         print(f"\n[{model}/{ckpt}] rel logit err over {len(rel)} images: worst {worst:.2e} "
               f"({names[int(rel.argmax())]}), p95 {np.percentile(rel, 95):.2e}, median {np.median(rel):.2e}, "
               f"> 1e-3: {int((rel > 1e-3).sum())}")
-        # reported, not asserted: flat logits inflate this relative measure (module docstring)
+        # flat logits inflate this relative measure (module docstring): the 1e-3 bar is asserted on
+        # the CLIP-scale fixtures; here a loose bound of twice the committed worst (1.42e-3, r03)
+        assert worst <= FLAT_TOL, (model, ckpt, worst, names[int(rel.argmax())])
         # per-segment argmax: identical unless the reference's top-1/top-2 margin is within
         # twice this image's absolute logit error
         off, exempt, checked = an.table.offsets, 0, 0
@@ -166,13 +177,15 @@ def test_flat_fixtures_results_match_reference_harness(gpu, golden_dir, images, 
         assert exempt <= 0.02 * checked
         # the result dicts (probabilities of 100*cos softmaxes: err in p <= ~ |dlogit|)
         paths = [str(golden_dir / "images" / n) for n in names]
-        eabs = np.abs(got - r).max(axis=1)
+        # the swap rule's error: the measured max |dlogit|, capped by the asserted bound
+        eabs = np.minimum(np.abs(got - r).max(axis=1), FLAT_TOL * np.abs(r).max(axis=1))
         rc = {}
         for flt, key in ((True, "filter_true"), (False, "filter_false")):
             res = an.analyze_images_batch(paths, batch_size=64, filter_interiors=flt, confidence_threshold=0.3)
             for i, (p, n) in enumerate(zip(paths, names)):
                 _compare(js[key][n], res[p], (model, ckpt, key, n), 2 * PROB_TOL, ref[i], js, logit_err=eabs[i], count=rc)
         print(f"[{model}/{ckpt}] result-dict near-tie label swaps: {rc}")
+        _swap_bound(rc, (model, ckpt, "flat result dicts"))
     finally:
         an.engine.close()
 
@@ -198,7 +211,7 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
     names, imgs = images
     assert js["images"] == names and js["detector_categories"] == L.DETECTOR_CATEGORIES
     an = InteriorAnalyzer(model=js["model"], device=0, categories=js["categories"], text_features=T,
-                          weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
+                          state_dict="synthetic", weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
                           lora_weights_path=str(golden_dir / "lora" / js["checkpoint"]))
     assert an.engine.compute_dtype == "fp16" and an.lora_report["loaded"] == 48
     try:
@@ -206,7 +219,8 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
         cols = _columns(js, an.table)
         r = ref[:, cols]
         rel = np.abs(got - r).max(axis=1) / np.abs(r).max(axis=1)
-        eabs = np.abs(got - r).max(axis=1)  # per-image max |dlogit| (absolute)
+        # per-image max |dlogit| (absolute), capped by the asserted 1e-3 bar
+        eabs = np.minimum(np.abs(got - r).max(axis=1), LOGIT_TOL * np.abs(r).max(axis=1))
         print(f"\n[{model}/{ckpt} clipscale] max|logit| median {np.median(np.abs(r).max(axis=1)):.1f}; "
               f"rel logit err worst {rel.max():.2e} ({names[int(rel.argmax())]}), p95 {np.percentile(rel, 95):.2e}, "
               f"median {np.median(rel):.2e}; abs err worst {eabs.max():.2e}")
@@ -219,6 +233,7 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
                 zr, zg = r[i, off[s]:off[s + 1]].astype(np.float64), got[i, off[s]:off[s + 1]]
                 pr = _softmax(zr)
                 k = min(5, len(zr))
+                cnt["checked"] = cnt.get("checked", 0) + k
                 for j, (a, b) in enumerate(zip(np.argsort(-zr)[:k], np.argsort(-zg)[:k])):
                     if a == b:
                         continue
@@ -231,6 +246,7 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
         print(f"[{model}/{ckpt} clipscale] ranking swaps (top-5 of {len(names) * (len(off) - 1)} segment rows): "
               f"prob gap < {GAP_TOL}: {cnt.get('gap', 0)}, logit gap within 2x measured error: {cnt.get('err', 0)}; "
               f"of them at rank 1: {top1}")
+        _swap_bound(cnt, (model, ckpt, "clipscale ranking"))
         paths = [str(golden_dir / "images" / n) for n in names]
         rc = {}
         for flt, key in ((True, "filter_true"), (False, "filter_false")):
@@ -266,6 +282,7 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
                 assert (pd["style"], pd["confidence"]) == tuple(pd["analysis"]["styles"][0]), n
                 assert pd["room_type"] == pd["analysis"]["room_types"][0][0], n
         print(f"[{model}/{ckpt} clipscale] result-dict / detector swaps: {rc}")
+        _swap_bound(rc, (model, ckpt, "clipscale result dicts"))
     finally:
         an.engine.close()
 
@@ -281,7 +298,7 @@ def test_text_caches_from_gpu_text_tower(gpu, golden_dir, images, ckpt):
     assert tok.vocab_size == facts["vocab"]
     text_sd = synthetic_text_state_dict(TextConfig(vocab=tok.vocab_size), facts["seed"])
     an = InteriorAnalyzer(model=js["model"], device=0, categories=js["categories"],
-                          weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
+                          state_dict="synthetic", weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
                           lora_weights_path=str(golden_dir / "lora" / js["checkpoint"]),
                           text_state_dict=text_sd, tokenizer=tok)
     try:
@@ -315,7 +332,7 @@ def test_logits_at_clip_scale_meet_bar_on_all_images(gpu, golden_dir, images, mo
     T = 0.3 * f_ref[np.arange(C_) % len(names)] + 0.95 * r
     T = (T / np.linalg.norm(T, axis=1, keepdims=True)).astype(np.float32)
     an = InteriorAnalyzer(model=js["model"], device=0, categories=js["categories"], text_features=T,
-                          weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
+                          state_dict="synthetic", weights_seed=js["weights_seed"], max_batch=64, use_lora=True,
                           lora_weights_path=str(golden_dir / "lora" / js["checkpoint"]))
     try:
         got = an.logits(imgs)

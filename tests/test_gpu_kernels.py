@@ -30,13 +30,14 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # 34xx / 35xx = column-group-major 1-D remap with 2 / 3 N-groups (tile_of_block).
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 13 / 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 60 / 61 the 256x256 ping-pong tile (gemm_pp.hip,
-# direct / LDS-staged 16-bit stores; 62 persistent, 63 the same with non-temporal stores);
+# direct / LDS-staged 16-bit stores; 62 persistent, 63 the same with non-temporal stores, 64 with
+# row-contiguous stores bounced through a per-wave LDS slot);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 13, 22, 60, 61, 62, 63, 80, 81, 82, 90, 98, 208, 213, 222, 260, 280, 282, 298, 3408, 3513, 3460,
-            3462, 3480]
+VARIANTS = [1, 2, 3, 8, 13, 22, 60, 61, 62, 63, 64, 80, 81, 82, 90, 98, 208, 213, 222, 260, 280, 282, 298, 3408, 3513,
+            3460, 3462, 3464, 3480]
 N128 = (1, 2, 13, 22, 81, 82)
-N256 = (3, 8, 60, 61, 62, 63, 80, 98)
-STAGED = (60, 61, 62, 63, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 60, 61, 62, 63, 64, 80, 98)
+STAGED = (60, 61, 62, 63, 64, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -51,7 +52,7 @@ def _skip(variant, N, K):
     v = variant % 100
     if (v in N128 and N % 128) or (v in N256 and N % 256):
         return "tile does not divide N"
-    if v in (60, 61, 62, 63) and K % 128:
+    if v in (60, 61, 62, 63, 64) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
     return None
 

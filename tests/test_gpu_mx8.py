@@ -166,8 +166,8 @@ def test_gemm_mx8_epilogues(gpu):
 
 
 # ---------------------------------------------------------------- end to end (config 5)
-def _engine(cfg, dtype, sd, adapters, T, segs, gpu, B):
-    eng = VisionEngine(cfg, gpu, dtype, max_batch=B)
+def _engine(cfg, dtype, sd, adapters, T, segs, gpu, B, tuning=None):
+    eng = VisionEngine(cfg, gpu, dtype, max_batch=B, tuning=tuning)
     eng.load_state_dict(sd)
     eng.load_lora(adapters)
     eng.set_text_features(T.numpy(), segs)
@@ -221,10 +221,10 @@ def test_mxfp8_logits_within_config5_bar(gpu):
 
 @pytest.mark.parametrize("model,skip,resid16", [("ViT-B/32", "", "1"), ("ViT-B/32", "0,1,10,11", "0"),
                                                ("ViT-B/16", None, None)])
-def test_mxfp8_forward_variants(gpu, monkeypatch, model, skip, resid16):
-    """The MX-fp8 forward's other block layouts: every block MX-fp8 (CLIPVIT_MX8_SKIP="": the last
+def test_mxfp8_forward_variants(gpu, model, skip, resid16):
+    """The MX-fp8 forward's other block layouts: every block MX-fp8 (tuning mx8_skip="": the last
     block runs on all rows, its c_proj adds into x in the MX GEMM epilogue, no class-token tail),
-    the fp32 read-modify-write residual adds (CLIPVIT_RESID16=0, the pre-r02 path), and the
+    the fp32 read-modify-write residual adds (resid16=0, the pre-r02 path), and the
     default layout on ViT-B/16 (N = 197). Against the bf16 engine at CLIP logit scale:
     embeddings aligned and logits within the all-MX-fp8 figure of DESIGN.md 5.7 (2.0e-2) plus
     margin."""
@@ -237,11 +237,12 @@ def test_mxfp8_forward_variants(gpu, monkeypatch, model, skip, resid16):
     px = torch.randn(B, 3, cfg.image_size, cfg.image_size, generator=g).clamp_(-1.8, 2.2).to(gpu)
     T0 = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
     e16 = _engine(cfg, "bf16", sd, adapters, T0, segs, gpu, B)
+    tun = {}
     if skip is not None:
-        monkeypatch.setenv("CLIPVIT_MX8_SKIP", skip)
+        tun["mx8_skip"] = skip
     if resid16 is not None:
-        monkeypatch.setenv("CLIPVIT_RESID16", resid16)
-    e8 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B)
+        tun["resid16"] = resid16
+    e8 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B, tuning=tun)
     try:
         f16 = e16.encode_image(px).cpu()
         anchor = torch.nn.functional.normalize(torch.nn.functional.normalize(f16, dim=-1).mean(0), dim=0)
@@ -253,16 +254,18 @@ def test_mxfp8_forward_variants(gpu, monkeypatch, model, skip, resid16):
         rel = ((l8 - l16).abs().amax(1) / l16.abs().amax(1)).max().item()
         cos = torch.nn.functional.cosine_similarity(r8.emb.cpu(), r16.emb.cpu(), dim=-1).min().item()
         print(f"mxfp8 {model} [skip {skip!r}, resid16 {resid16}] vs bf16: max rel logit err {rel:.4g}, min emb cosine {cos:.6f}")
-        assert cos > 0.99 and rel <= 3e-2, (rel, cos)
+        # the shipped default layout (skip None) meets the config-5 bar; the alternative layouts
+        # are held to the all-MX-fp8 figure of DESIGN.md 5.7 (2.0e-2) plus margin
+        assert cos > 0.99 and rel <= (2e-2 if skip is None and resid16 is None else 3e-2), (rel, cos)
     finally:
         e16.close()
         e8.close()
 
 
-def test_attention_q8_output_bit_identical(gpu, monkeypatch):
+def test_attention_q8_output_bit_identical(gpu):
     """The MX-fp8 forward's attention writes the out_proj operand (MX-fp8) in its epilogue
     (ViT-B/32, N = 50): embeddings and logits must equal those of the two-kernel path
-    (16-bit attention output + launch_quant_mx8, CLIPVIT_ATTN_Q8=0) bit for bit."""
+    (16-bit attention output + launch_quant_mx8, tuning attn_q8=0) bit for bit."""
     cfg = C.get_config("ViT-B/32")
     sd = synthetic_state_dict(cfg, 0)
     adapters = synthetic_adapters(cfg, rank=8)
@@ -272,8 +275,7 @@ def test_attention_q8_output_bit_identical(gpu, monkeypatch):
     px = torch.randn(B, 3, 224, 224, generator=g).clamp_(-1.8, 2.2).to(gpu)
     T = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
     fused = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B)
-    monkeypatch.setenv("CLIPVIT_ATTN_Q8", "0")
-    split = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B)
+    split = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B, tuning={"attn_q8": 0})
     try:
         a, b = fused.classify(px), split.classify(px)
         assert torch.equal(a.emb, b.emb)
@@ -283,8 +285,8 @@ def test_attention_q8_output_bit_identical(gpu, monkeypatch):
         split.close()
 
 
-def test_fp16_residual_stream_within_config5_bar(gpu, monkeypatch):
-    """MX-fp8 forward with the fp16 residual stream (the default, CLIPVIT_X16) and with the fp32
+def test_fp16_residual_stream_within_config5_bar(gpu):
+    """MX-fp8 forward with the fp16 residual stream (the default, tuning x16) and with the fp32
     one, both against the bf16 engine at CLIP logit scale. The two MX-fp8 forwards differ by
     ~1.5e-2 from each other (any perturbation flips e4m3 roundings of the GEMM operands: the same
     size as the MX-fp8 error itself), so the check is on the error against bf16: the fp16 stream
@@ -300,8 +302,7 @@ def test_fp16_residual_stream_within_config5_bar(gpu, monkeypatch):
     T0 = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
     e16 = _engine(cfg, "bf16", sd, adapters, T0, segs, gpu, B)
     x16 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B)
-    monkeypatch.setenv("CLIPVIT_X16", "0")
-    x32 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B)
+    x32 = _engine(cfg, "mxfp8", sd, adapters, T0, segs, gpu, B, tuning={"x16": 0})
     try:
         f = e16.encode_image(held).cpu()
         anchor = torch.nn.functional.normalize(torch.nn.functional.normalize(f, dim=-1).mean(0), dim=0)
@@ -319,3 +320,56 @@ def test_fp16_residual_stream_within_config5_bar(gpu, monkeypatch):
         e16.close()
         x16.close()
         x32.close()
+
+
+def test_config5_bs512_as_benched(gpu):
+    """BASELINE config 5 exactly as bench.py --dtype mxfp8 --batch 512 runs it: ViT-B/32 + merged
+    LoRA r=8, 512 images in one classify, which takes the two-lane split (256 images per lane
+    stream) and the shipped MX-fp8 tiles (mx8_variants default) and bf16 block masks. Text rows
+    at CLIP logit scale, built as tests/golden/make_golden.py clip_scale_text builds them
+    (normalise(0.3 f + 0.95 r), f = the oracle's fp32 features of 16 of the images). Asserted:
+    every one of the 512 images within 2e-2 of the bf16 engine (BASELINE's bar), 4 sample rows
+    from both lanes within 2e-2 of the CPU fp32 oracle, and the two-lane split bit-identical to
+    one stream (main.py:440-448 batches the same way)."""
+    from oracle import clip_ref
+    cfg = C.get_config("ViT-B/32")
+    sd = synthetic_state_dict(cfg, 0)
+    adapters = synthetic_adapters(cfg, rank=8)
+    g = torch.Generator().manual_seed(512)
+    segs = [0, 40, 60, 359, 395, 425, 437]
+    B = 512
+    px = torch.randn(B, 3, 224, 224, generator=g).clamp_(-1.8, 2.2)
+    ref_sd = dict(sd)
+    for a in adapters:
+        ref_sd[a.target] = clip_ref.merge_lora(sd[a.target], torch.from_numpy(a.A), torch.from_numpy(a.B), a.scaling)
+    probe = [0, 255, 256, 511] + list(range(1, 13))  # both lanes' first / last images first
+    with torch.no_grad():
+        f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[probe])
+    gen = torch.Generator().manual_seed(2024)
+    fn = torch.nn.functional.normalize(f_ref, dim=-1).double()
+    r = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=gen, dtype=torch.float64), dim=-1)
+    T = 0.3 * fn[torch.arange(437) % fn.shape[0]] + 0.95 * r
+    T = (T / T.norm(dim=-1, keepdim=True)).float()
+    pxg = px.to(gpu)
+    e16 = _engine(cfg, "bf16", sd, adapters, T, segs, gpu, B)
+    e8 = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B)
+    one = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, B, tuning={"split_min": 0})
+    try:
+        l16 = e16.classify(pxg).logits.cpu()
+        r8 = e8.classify(pxg)
+        l8 = r8.logits.cpu()
+        ro = one.classify(pxg)
+        torch.cuda.synchronize()
+        assert torch.equal(r8.logits, ro.logits) and torch.equal(r8.emb, ro.emb)
+        rel = ((l8 - l16).abs().amax(1) / l16.abs().amax(1))
+        _, lo, _, _, _ = clip_ref.head(f_ref[:4], T, segs)
+        rel_o = ((l8[probe[:4]] - lo).abs().amax(1) / lo.abs().amax(1))
+        print(f"config 5 bs 512 (split, shipped MX tiles): vs bf16 worst {rel.max():.4g} median "
+              f"{rel.median():.4g}; vs oracle rows {probe[:4]}: {rel_o.max():.4g}; "
+              f"max |logit| median {l16.abs().amax(1).median():.1f}")
+        assert rel.max().item() <= 2e-2, rel.max().item()
+        assert rel_o.max().item() <= 2e-2, rel_o.max().item()
+    finally:
+        e16.close()
+        e8.close()
+        one.close()

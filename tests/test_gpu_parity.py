@@ -132,8 +132,8 @@ def test_encode_image_unnormalised(gpu):
     assert torch.nn.functional.cosine_similarity(f, ref).min() > 0.9995
 
 
-def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
-    """The two-stream split (default from 12,800 tokens per batch; CLIPVIT_SPLIT_MIN) computes every image with the same
+def test_two_lane_split_is_bit_identical(gpu):
+    """The two-stream split (default from 12,800 tokens per batch; tuning split_min) computes every image with the same
     kernels and k-order, so its outputs equal the single-stream outputs bit for bit."""
     cfg = C.VIT_B32
     sd = synthetic_state_dict(cfg, 0)
@@ -142,8 +142,7 @@ def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
     px = _pixels(96, 224, seed=21).to(gpu)
     outs = []
     for split in ("0", "64"):
-        monkeypatch.setenv("CLIPVIT_SPLIT_MIN", split)
-        eng = VisionEngine(cfg, 0, "fp16", max_batch=128)
+        eng = VisionEngine(cfg, 0, "fp16", max_batch=128, tuning={"split_min": split})
         eng.load_state_dict(sd)
         eng.set_text_features(T.numpy(), seg)
         o = eng.classify(px)
@@ -157,17 +156,16 @@ def test_two_lane_split_is_bit_identical(gpu, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
-def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
-    """The deferred residual store (CLIPVIT_DEFER_X) executes the same per-row fp32 operations in
+def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, dtype):
+    """The deferred residual store (tuning defer_x) executes the same per-row fp32 operations in
     the same order, so the features equal the full computation's bit for bit (B/32 and the
-    N = 197 B/16 geometry), with the last block on class-token rows only (CLIPVIT_CLS_PRUNE) and
-    without, with the LayerNorm fold (CLIPVIT_LNFOLD) and without. The unfolded class-token tail
+    N = 197 B/16 geometry), with the last block on class-token rows only (cls_prune) and
+    without, with the LayerNorm fold (lnfold) and without. The unfolded class-token tail
     splits K of its three GEMMs (fp32 partials summed in slice order, no 16-bit branch output),
     so pruned and full last blocks agree to rounding; the folded tail stays bit-identical. The
     folded and unfolded paths agree to rounding (different but equivalent arithmetic). The
-    identities hold for the fp32 residual stream (CLIPVIT_X24=0); the default 24-bit stream
+    identities hold for the fp32 residual stream (x24=0); the default 24-bit stream
     (pruned + deferred path) is compared with it to rounding."""
-    monkeypatch.setenv("CLIPVIT_X24", "0")
     for cfg, B in ((C.VIT_B32, 67), (C.VIT_B16, 9)):
         sd = synthetic_state_dict(cfg, 0)
         ad = synthetic_adapters(cfg, rank=8)
@@ -175,13 +173,11 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
         groups = {}
         for fold, prune, defer in (("1", "0", "0"), ("1", "1", "0"), ("0", "0", "0"), ("0", "1", "1"),
                                    ("0", "1", "0"), ("0", "0", "1")):
-            monkeypatch.setenv("CLIPVIT_LNFOLD", fold)
-            monkeypatch.setenv("CLIPVIT_CLS_PRUNE", prune)
-            monkeypatch.setenv("CLIPVIT_DEFER_X", defer)
-            eng = VisionEngine(cfg, 0, dtype, max_batch=B)
+            eng = VisionEngine(cfg, 0, dtype, max_batch=B,
+                               tuning={"x24": 0, "lnfold": fold, "cls_prune": prune, "defer_x": defer})
             eng.load_state_dict(sd)
             eng.load_lora(ad)
-            # the fold applies to the fp16 path only (bf16 ignores CLIPVIT_LNFOLD)
+            # the fold applies to the fp16 path only (bf16 ignores lnfold)
             key = "fold" if fold == "1" and dtype == "fp16" else "prune" + prune
             groups.setdefault(key, []).append(eng.encode_image(px).clone())
             torch.cuda.synchronize()
@@ -200,11 +196,7 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
             f1, f0 = groups["fold"][0], groups["prune0"][0]
             assert rel(f1, f0) < 3e-3, (cfg.name, dtype, rel(f1, f0))
         # the 24-bit residual stream (default): x rounded to a 16-bit significand at every store
-        monkeypatch.setenv("CLIPVIT_X24", "1")
-        monkeypatch.setenv("CLIPVIT_CLS_PRUNE", "1")
-        monkeypatch.setenv("CLIPVIT_DEFER_X", "1")
-        monkeypatch.setenv("CLIPVIT_LNFOLD", "0")
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B)
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B)  # shipped defaults: x24, cls_prune, defer_x
         eng.load_state_dict(sd)
         eng.load_lora(ad)
         f24 = eng.encode_image(px).clone()
@@ -212,7 +204,6 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, monkeypatch, dtype):
         d24 = rel(f24, groups["prune1"][0])
         print(f"[{cfg.name} {dtype}] 24-bit vs fp32 residual stream: rel {d24:.2e}")
         assert 0 < d24 < (1.5e-3 if dtype == "fp16" else 1e-2), (cfg.name, dtype, d24)
-        monkeypatch.setenv("CLIPVIT_X24", "0")
 
 
 @pytest.mark.parametrize("dtype,pdt", [("fp16", torch.float16), ("bf16", torch.bfloat16)])
@@ -309,7 +300,7 @@ def test_full_batch_256_properties(gpu, dtype):
     _check_logits(full[idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[(dtype, "peaked")])
 
 
-def test_config4_l14_336_bs128_as_benched(gpu, monkeypatch):
+def test_config4_l14_336_bs128_as_benched(gpu):
     """BASELINE config 4 exactly as bench.py runs it: ViT-L/14@336 + merged LoRA r=16, fp16, 128
     images in one classify, which takes the two-lane half-batch split (64 images per lane stream)
     and the 256x256 v80 tiles of every role. A sample of rows from both lanes against the oracle
@@ -324,11 +315,7 @@ def test_config4_l14_336_bs128_as_benched(gpu, monkeypatch):
     seg = [0, 40, 60, 359, 395, 425, 437]
     outs = {}
     for split in ("default", "0"):
-        if split == "default":
-            monkeypatch.delenv("CLIPVIT_SPLIT_MIN", raising=False)
-        else:
-            monkeypatch.setenv("CLIPVIT_SPLIT_MIN", split)
-        eng = VisionEngine(cfg, 0, "fp16", max_batch=128)
+        eng = VisionEngine(cfg, 0, "fp16", max_batch=128, tuning=None if split == "default" else {"split_min": split})
         eng.load_state_dict(sd)
         eng.load_lora(ad)
         eng.set_text_features(T.numpy(), seg)
@@ -343,3 +330,32 @@ def test_config4_l14_336_bs128_as_benched(gpu, monkeypatch):
     _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
     rel = _check_logits(outs["default"][0][idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[("fp16", "peaked")])
     print(f"L/14@336 bs 128 (split + v80 tiles): max rel logit err {rel:.2e} on rows {idx}")
+
+
+def test_lnfold_bs256_runs_through_the_round_split(gpu):
+    """the LayerNorm-fold path (tuning lnfold=1) at the headline batch, B/32 bs 256,
+    where c_fc's 600 tiles take the whole-round row split. The ping-pong main tiles have only the
+    16-bit STORE / GELU epilogues, so the folded c_fc (EPI_LNF_GELU) must take the single-launch
+    path instead of failing. Rows from the start, middle and end of the batch against the oracle
+    at the 1e-3 bar (peaked text)."""
+    cfg = C.VIT_B32
+    sd = synthetic_state_dict(cfg, 0)
+    ad = synthetic_adapters(cfg, rank=8)
+    ref_sd = _merged(sd, ad)
+    px = _pixels(256, 224, seed=43)
+    T = _text(cfg.embed_dim, 437, anchor=_anchor(ref_sd, cfg.name, 224))
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    eng = VisionEngine(cfg, 0, "fp16", max_batch=256, tuning={"lnfold": 1})
+    try:
+        eng.load_state_dict(sd)
+        eng.load_lora(ad)
+        eng.set_text_features(T.numpy(), seg)
+        o = eng.classify(px.to(gpu))
+        torch.cuda.synchronize()
+        idx = [0, 127, 214, 255]  # 214: a row of c_fc's tail launch (rows >= 10,752 = image 215)
+        f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[idx])
+        _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
+        rel = _check_logits(o.logits[idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[("fp16", "peaked")])
+        print(f"B/32 bs 256 lnfold: max rel logit err {rel:.2e}")
+    finally:
+        eng.close()

@@ -189,7 +189,7 @@ def test_gpu_analyzer_label_matrix_from_text_tower(gpu, tok, golden_dir, tmp_pat
             ck[k + "lora_B"] = torch.randn(4, o_f, generator=g) * 0.02
     path = tmp_path / "comprehensive_lora.pth"
     torch.save(ck, path)
-    an = InteriorAnalyzer("ViT-B/32", use_lora=True, lora_weights_path=str(path), lora_rank=4,
+    an = InteriorAnalyzer("ViT-B/32", state_dict="synthetic", use_lora=True, lora_weights_path=str(path), lora_rank=4,
                           lora_alpha=8, device=gpu, compute_dtype="fp16",
                           dataset_json=golden_dir / "interior_dataset.json", max_batch=4,
                           text_state_dict=sd, tokenizer=tok)

@@ -42,8 +42,8 @@ def test_in_memory_database_interface():
 @pytest.mark.gpu
 def test_gpu_apartment_pipeline(gpu, golden_dir):
     from interior_amd.analyzer import InteriorAnalyzer
-    an = InteriorAnalyzer("ViT-B/32", device=gpu, compute_dtype="fp16", max_batch=8,
-                          dataset_json=golden_dir / "interior_dataset.json",
+    an = InteriorAnalyzer("ViT-B/32", state_dict="synthetic", text_features="synthetic", device=gpu,
+                          compute_dtype="fp16", max_batch=8, dataset_json=golden_dir / "interior_dataset.json",
                           extra_segments=W.worker_style_segment())
     files = sorted((golden_dir / "images").glob("*.jpg"))[::12]  # 13 of the 151 fixture photos
     rng = np.random.default_rng(0)

@@ -1,13 +1,12 @@
 """Config 5: MX-fp8 logit error against the bf16 engine for several sets of bf16 blocks
-(CLIPVIT_MX8_SKIP), at the CLIP logit scale of tests/test_gpu_mx8.py (peaked text rows) and on
+(tuning mx8_skip), at the CLIP logit scale of tests/test_gpu_mx8.py (peaked text rows) and on
 random text rows; several seeds of images and text.
 
     python tools/mx_skip_sweep.py "0,1,10,11" "0,10,11" "11|0,1,10,11" ...
 
 An argument "A|M" keeps the attention roles (QKV, out_proj) of blocks A and the MLP roles of
-blocks M in bf16 (CLIPVIT_MX8_SKIP / CLIPVIT_MX8_SKIP_MLP); a plain list sets both.
+blocks M in bf16 (tuning mx8_skip / mx8_skip_mlp); a plain list sets both.
 """
-import os
 import sys
 from pathlib import Path
 
@@ -31,8 +30,8 @@ def peaked(anchor, seed, a=0.3):
     return torch.nn.functional.normalize(a * anchor[None, :] + (1 - a * a) ** 0.5 * T, dim=-1)
 
 
-def engine(cfg, dtype, sd, ad, B, dev):
-    e = VisionEngine(cfg, dev, dtype, max_batch=B)
+def engine(cfg, dtype, sd, ad, B, dev, tuning=None):
+    e = VisionEngine(cfg, dev, dtype, max_batch=B, tuning=tuning)
     e.load_state_dict(sd)
     e.load_lora(ad)
     return e
@@ -59,12 +58,10 @@ def main():
             cases.append((seed, name, px, T, e16.classify(px).logits.cpu()))
     for skip in sys.argv[1:]:
         att, _, mlp = skip.partition("|")
-        os.environ["CLIPVIT_MX8_SKIP"] = att
+        tun = {"mx8_skip": att}
         if mlp:
-            os.environ["CLIPVIT_MX8_SKIP_MLP"] = mlp
-        else:
-            os.environ.pop("CLIPVIT_MX8_SKIP_MLP", None)
-        e8 = engine(cfg, "mxfp8", sd, ad, B, dev)
+            tun["mx8_skip_mlp"] = mlp
+        e8 = engine(cfg, "mxfp8", sd, ad, B, dev, tuning=tun)
         res = {"peaked": [], "random": []}
         for seed, name, px, T, ref in cases:
             e8.set_text_features(T.numpy(), SEGS)
