@@ -77,6 +77,12 @@ struct Lane {
     float2* st = nullptr;  // lnfold: [cap*N, D/128] per-row 128-column (mean, M2) of x
     unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
     void* x16 = nullptr;  // MX-fp8 mode: [cap*N, D] fp16 residual stream (handle x16)
+    // stream-K GEMM workspace (gemm_pp.hip variant 65): fp32 partial slots [ncu][256 KB] and
+    // flags [ncu + 1][8]; sk_epoch counts this lane's stream-K launches (flags equal to it are
+    // the current launch's: the lane's launches are ordered on its stream)
+    void* sk_part = nullptr;
+    unsigned* sk_flag = nullptr;
+    unsigned sk_epoch = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
 };
@@ -236,6 +242,13 @@ struct clipvit_handle {
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
     // ms per forward, main-launch traffic 1.59x -> 1.38x of algorithmic
     int split_xcd = 34;
+    // stream-K GEMM (gemm_pp.hip variant 65) for these roles (bit = Role; tuning stream_k): one
+    // launch in which every CU owns an equal share of the k-tile iterations, in place of the
+    // whole-round row split. Off: measured 94.8 us against 77.3 (one launch) and 73.7 (row split)
+    // for c_fc at bs 256 — the shares start at different k, so workgroups that share an operand
+    // panel need its k-slices at different times and the L2 working set becomes whole panels
+    // (2.5 us per k-tile against 1.7)
+    unsigned sk_roles = 0;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -280,6 +293,8 @@ static int free_ws(Workspace* w) {
         hipFree(l.st);
         hipFree(l.q8);
         hipFree(l.x16);
+        hipFree(l.sk_part);
+        hipFree(l.sk_flag);
         if (l.done) hipEventDestroy(l.done);
         if (l.stream) hipStreamDestroy(l.stream);
     }
@@ -311,6 +326,11 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
         if (e == hipSuccess && h->mx8) e = hipMalloc(&l.x16, rows * h->D * 2);
         else if (e == hipSuccess && h->use_x24()) e = hipMalloc(&l.x16, rows * h->D * 3);
+        if (e == hipSuccess && h->sk_roles) {
+            e = hipMalloc(&l.sk_part, (size_t)h->ncu * 256 * 256 * 4);
+            if (e == hipSuccess) e = hipMalloc((void**)&l.sk_flag, (size_t)(h->ncu + 1) * 8 * 4);
+            if (e == hipSuccess) e = hipMemset(l.sk_flag, 0, (size_t)(h->ncu + 1) * 8 * 4);
+        }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
     }
@@ -393,7 +413,8 @@ struct Fold {
 };
 
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
-                const float* bias, void* C, int M, int N, int K, int ldc, int role, const Fold& fo = Fold()) {
+                const float* bias, void* C, int M, int N, int K, int ldc, int role, const Fold& fo = Fold(),
+                Lane* lane = nullptr) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
@@ -418,6 +439,20 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the main launch's tile width: every pipelined variant a round split can use is 256 wide
     // (8 / 80: 256x256, 98: 240x256)
     const int bn = 256;
+    // stream-K: one launch, every CU the same share of k-tiles (the role's 16-bit STORE / GELU
+    // epilogue; falls through when a share would cover less than one tile's k-tiles)
+    if (lane && lane->sk_part && ((h->sk_roles >> role) & 1) && !h->var_forced && t256 &&
+        t256 >= h->ncu && t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
+        GemmArgs b = a;
+        b.xcd_n = h->split_xcd;
+        if (xcd_split_n(N / 256, b.xcd_n)) b.xcd_n = 0;
+        b.sk_part = lane->sk_part;
+        b.sk_flag = lane->sk_flag;
+        b.sk_epoch = ++lane->sk_epoch;
+        if (b.sk_epoch == 0) b.sk_epoch = ++lane->sk_epoch;  // 0 = a never-written flag
+        if (launch_gemm(s, h->dt, epi, b, 65) == 0) return 0;
+        --lane->sk_epoch;
+    }
     // (the ping-pong main tiles, split_main >= 60, have the 16-bit STORE / GELU epilogues only:
     // the LayerNorm-fold epilogues take the single-launch path below)
     const bool split_epi = epi == EPI_STORE || epi == EPI_GELU ||
@@ -605,7 +640,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         // q: the attention roles (QKV, out_proj) in MX-fp8; qm: the MLP roles
         const bool q = h->q8_attn(i), qm = h->q8_mlp(i), last = i + 1 == h->cfg.layers;
         rc = q ? gemm8(s, h, EPI_STORE, q8, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)
-               : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV);
+               : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w);
         if (rc) return rc;
         if (prof) prof->mark(s, F_QKV);
         if (!q || !h->attn_q8 || launch_attention_q8(s, h->dt, w->qkv, q8, q8s, B, N, h->cfg.heads) != 0) {
@@ -629,7 +664,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         else ln(ly.ln2g, ly.ln2b, qm);
         if (prof) prof->mark(s, F_LN);
         rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
-               : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC);
+               : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w);
         if (rc) return rc;
         if (prof) prof->mark(s, F_FC);
         const bool p16 = r16 && !last;
@@ -771,7 +806,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
         const bool last = i + 1 == nl;
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
@@ -793,7 +828,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
         }
         if (prof) prof->mark(s, F_LN);
-        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC)))
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w)))
             return rc;
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
@@ -1044,7 +1079,10 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     } else if (k == "mx8_skip_mlp") ok = parse_mask(v, h->mx8_skip_mlp);
     else if (k == "mx8_variants") ok = parse_list(v, h->var8, 4);
     else if (k == "large_variants") ok = parse_list(v, h->large_var, 4);
-    else if (k == "gemm_variants") {
+    else if (k == "stream_k") {  // role bit mask (1 QKV, 4 c_fc); 0 = off
+        ok = parse_int(v, x) && x >= 0;
+        if (ok) h->sk_roles = (unsigned)x;
+    } else if (k == "gemm_variants") {
         ok = parse_list(v, h->var, 5);
         h->var_forced = ok;
     } else FAIL(CLIPVIT_E_INVALID, "unknown tuning key '" + k + "'");
@@ -1076,11 +1114,12 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
         int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
+        unsigned sk_roles;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
               g->var_forced, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
-              g->split_min, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
+              g->split_min, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
         memcpy(t.large_var, g->large_var, sizeof t.large_var);
@@ -1102,6 +1141,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             memcpy(h->var, before.var, sizeof before.var);
             h->mx8_skip = before.mx8_skip;
             h->mx8_skip_mlp = before.mx8_skip_mlp;
+            h->sk_roles = before.sk_roles;
             return rc;
         }
     }
@@ -1438,6 +1478,22 @@ static int current_ncu() {
     return n;
 }
 
+// stream-K workspace for the kernel-level entry points (variant 65): fresh buffers, epoch 1
+struct SkScratch {
+    void* part = nullptr;
+    unsigned* flag = nullptr;
+    ~SkScratch() {
+        if (part) (void)hipFree(part);
+        if (flag) (void)hipFree(flag);
+    }
+    int alloc(int ncu) {
+        const int n = ncu > 0 ? ncu : 256;
+        if (hipMalloc(&part, (size_t)n * 256 * 256 * 4) != hipSuccess) return -1;
+        if (hipMalloc((void**)&flag, (size_t)(n + 1) * 8 * 4) != hipSuccess) return -1;
+        return hipMemset(flag, 0, (size_t)(n + 1) * 8 * 4) == hipSuccess ? 0 : -1;
+    }
+};
+
 int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi, int variant) {
     g_err.clear();
@@ -1454,11 +1510,19 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.ncu = current_ncu();
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
+    SkScratch sk;
+    if (variant == 65) {
+        HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+        if (sk.alloc(a.ncu)) FAIL(CLIPVIT_E_NOMEM, "stream-K workspace");
+        a.sk_part = sk.part;
+        a.sk_flag = sk.flag;
+        a.sk_epoch = 1;
+    }
     int rc;
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 60 ||
-                        variant == 61 || variant == 62 || variant == 63 || variant == 64;
+                        variant == 61 || variant == 62 || variant == 63 || variant == 64 || variant == 65;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;
@@ -1480,6 +1544,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         rc = launch_gemm(s, dtype, e, a, variant);
     }
     HIPCHK(hipFreeAsync(Wp, s));
+    if (variant == 65) HIPCHK(hipStreamSynchronize(s));  // before the workspace is freed
     if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
     HIPCHK(hipGetLastError());
     return 0;
@@ -1562,6 +1627,13 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.ncu = current_ncu();
     // diagnostic: persistent GEMMs on fewer workgroups (store-burst experiments)
     if (const char* v = getenv("CLIPVIT_BENCH_GRID")) a.ncu = atoi(v);
+    SkScratch sk;
+    if (variant == 65) {
+        if (sk.alloc(a.ncu)) FAIL(CLIPVIT_E_NOMEM, "stream-K workspace");
+        a.sk_part = sk.part;
+        a.sk_flag = sk.flag;
+        a.sk_epoch = 0;
+    }
     int e = epi;  // raw Epi enum
     if (mx) {
         a.sA = (const unsigned char*)A + (size_t)M * K;
@@ -1570,6 +1642,7 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
         if (e == EPI_GELU) e = EPI_GELU_Q8;
     }
     auto launch = [&]() {
+        ++a.sk_epoch;  // stream-K: a fresh epoch per launch
         return mx ? launch_gemm_mx8(nullptr, CLIPVIT_BF16, e, a, variant) : launch_gemm(nullptr, dtype, e, a, variant);
     };
     int rc = launch();
@@ -1585,6 +1658,26 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     hipEventDestroy(t0);
     hipEventDestroy(t1);
     *avg_ms = ms / iters;
+    if (variant == 65 && !rc && getenv("CLIPVIT_SK_TRACE")) {  // diagnostic: one traced launch
+        const int G = a.ncu > 0 ? a.ncu : 256;
+        unsigned long long* tr = nullptr;
+        if (hipMalloc((void**)&tr, (size_t)G * 8 * 8) == hipSuccess) {
+            (void)hipMemset(tr, 0, (size_t)G * 8 * 8);
+            a.sk_trace = tr;
+            rc = launch();
+            std::vector<unsigned long long> t((size_t)G * 8);
+            (void)hipMemcpy(t.data(), tr, t.size() * 8, hipMemcpyDeviceToHost);
+            (void)hipFree(tr);
+            a.sk_trace = nullptr;
+            unsigned long long t0 = ~0ull;
+            for (int p = 0; p < G; ++p) t0 = std::min(t0, t[p * 8]);
+            for (int p = 0; p < G; p += (p < 16 ? 1 : 16)) {
+                printf("sk wg %3d:", p);
+                for (int i = 0; i < 8; ++i) printf(" %7.2f", t[p * 8 + i] ? (t[p * 8 + i] - t0) * 0.01 : -1.0);
+                printf("  (us: start, job ends 1-5, late wait start/end)\n");
+            }
+        }
+    }
     hipFree(A);
     hipFree(W);
     hipFree(Cb);

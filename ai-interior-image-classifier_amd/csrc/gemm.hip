@@ -826,7 +826,7 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (variant >= 60 && variant <= 64) return launch_gemm_pp(s, dtype, epi, a, variant);
+    if (variant >= 60 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);

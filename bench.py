@@ -203,16 +203,21 @@ def parity_config5(eng, px, T_rand, cfg, dev, n: int = 64, n_oracle: int = 4):
     return out
 
 
+DEFAULT_PROFILE = ROOT / "profiles" / "r04_fc_traffic.json"  # committed by tools/profile_round.sh
+
+
 def load_traffic(path: str | None):
-    """HBM bytes per c_fc launch from a rocprofv3 PMC pass of this same command (tools/
-    profile_round.sh writes it and passes --traffic-json): (bytes, source) or (None, None)."""
-    if not path:
-        return None, None
+    """The c_fc figures of a rocprofv3 profile of this same command (tools/profile_round.sh: kernel
+    trace + separate PMC passes; it passes --traffic-json to its own bench run). Without the flag,
+    the committed profile of the current build (DEFAULT_PROFILE), labelled as such. Returns
+    (dict or None, source)."""
+    p = Path(path) if path else DEFAULT_PROFILE
     try:
-        d = json.loads(Path(path).read_text())
-        return d.get("fc_gemm_bytes_per_launch"), d.get("source", path)
+        d = json.loads(p.read_text())
     except (OSError, ValueError):
         return None, None
+    src = d.get("source", str(p))
+    return d, (src if path else f"committed profile ({src}), not this run")
 
 
 def reconcile(fam: dict, step_ms: float):
@@ -339,7 +344,14 @@ def main():
     gflop_img = cfg.gflop_per_image() - pruned
     model_tflops = value / world * gflop_img / 1e3
 
-    traffic, traffic_src = load_traffic(a.traffic_json)
+    prof, traffic_src = load_traffic(a.traffic_json)
+    traffic = prof.get("fc_gemm_bytes_per_launch") if prof else None
+    rocprof = None
+    if prof and prof.get("fc_gemm_avg_us"):  # the rocprof figure beside this line's event timing
+        rocprof = {"avg_launch_us": round(prof["fc_gemm_avg_us"], 2),
+                   "frac": round(mlp_flop / (prof["fc_gemm_avg_us"] * 1e-6) / 1e12 / PEAK_TFLOPS["fp16"], 4),
+                   "mfma_busy": prof.get("fc_gemm_mfma_busy"), "l2_hit": prof.get("fc_gemm_l2_hit"),
+                   "wait_share": prof.get("fc_gemm_wait_share"), "source": traffic_src}
     cast_ms = 0.0
     if px.dtype != torch.float32:  # the fp32 -> 16-bit cast encode_image does, left out here
         cast_ms = eng.profile_forward(px.float(), iters=a.profile_iters)["patch_embed"] - fam["patch_embed"]
@@ -367,7 +379,10 @@ def main():
                    **({"tuning": a.tuning} if a.tuning else {})},
         "roofline": {"bound": "mfma", "kernel": "c_fc GEMM (+QuickGELU), the largest kernel family",
                      "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "frac": round(achieved / peak, 4), "timing": "HIP events on the launch stream (reconciled)",
+                     "rocprof": rocprof if a.dtype == "fp16" and a.batch == 256 and cfg.name == "ViT-B/32" else None,
+                     "traffic": traffic if a.dtype == "fp16" and a.batch == 256 and cfg.name == "ViT-B/32" else None,
+                     "traffic_source": traffic_src,
                      "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(fc_ms, 5),
                      "mlp_pair_frac": round(mlp_flop / (mlp_ms * 1e-3) / 1e12 / peak, 4),
                      "model_mfma_frac": round(model_tflops / peak, 4),

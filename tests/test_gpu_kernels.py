@@ -31,13 +31,15 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 13 / 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 60 / 61 the 256x256 ping-pong tile (gemm_pp.hip,
 # direct / LDS-staged 16-bit stores; 62 persistent, 63 the same with non-temporal stores, 64 with
-# row-contiguous stores bounced through a per-wave LDS slot);
+# row-contiguous stores bounced through a per-wave LDS slot; 65 stream-K: every CU an equal share
+# of the k-tile iterations, split tiles combined through fp32 partial slots; whole tiles where a
+# share would be shorter than one tile's k-tiles);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 13, 22, 60, 61, 62, 63, 64, 80, 81, 82, 90, 98, 208, 213, 222, 260, 280, 282, 298, 3408, 3513,
-            3460, 3462, 3464, 3480]
+VARIANTS = [1, 2, 3, 8, 13, 22, 60, 61, 62, 63, 64, 65, 80, 81, 82, 90, 98, 208, 213, 222, 260, 280, 282, 298, 3408,
+            3513, 3460, 3462, 3464, 3465, 3480]
 N128 = (1, 2, 13, 22, 81, 82)
-N256 = (3, 8, 60, 61, 62, 63, 64, 80, 98)
-STAGED = (60, 61, 62, 63, 64, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 60, 61, 62, 63, 64, 65, 80, 98)
+STAGED = (60, 61, 62, 63, 64, 65, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -52,7 +54,7 @@ def _skip(variant, N, K):
     v = variant % 100
     if (v in N128 and N % 128) or (v in N256 and N % 256):
         return "tile does not divide N"
-    if v in (60, 61, 62, 63, 64) and K % 128:
+    if v in (60, 61, 62, 63, 64, 65) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
     return None
 
@@ -73,6 +75,31 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     ref = _ref_gemm(A, W, bias, 0)
     err = (C - ref).abs().max().item() / ref.abs().max().item()
     assert err < _tol(variant, dtype), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("epi", [10, 11])
+@pytest.mark.parametrize("variant", [65, 3465])
+@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768),    # B/32 c_fc at bs 256: 28-29 k-tiles per CU
+                                   (12763, 3072, 768),    # ragged last row tile
+                                   (9000, 2304, 1024),    # 20-21 of 16 k-tiles, ragged
+                                   (8000, 2304, 1536),    # nk 24: 27 per CU, shares just above a tile
+                                   (4096, 4096, 1024)])   # one whole tile per CU (no split)
+def test_gemm_stream_k(gpu, dtype, epi, variant, M, N, K):
+    """Stream-K (variant 65): tiles split between two CUs are combined through the fp32 partial
+    slots (EARLY suffix stored with sc1 write-through stores, LATE prefix accumulated on top of
+    the loaded partial). Every output element against the fp32 reference (16-bit output), and two
+    launches bit-identical (the partition, hence the arithmetic, is fixed by the shape)."""
+    g = torch.Generator(device=gpu).manual_seed(M + N + K + epi)
+    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(N, device=gpu, generator=g)
+    C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
+    C2 = E.gemm_test(A, W, bias, epi=epi, variant=variant)
+    ref = _ref_gemm(A, W, bias, epi - 10)
+    err = (C - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (8e-3 if dtype == torch.bfloat16 else 2e-3), err
+    assert torch.equal(C, C2)
 
 
 @pytest.mark.parametrize("variant", STAGED + (8, 13, 22))

@@ -142,9 +142,14 @@ def main():
     for r, role, solo in zip(trace, roles, iso):
         (dur if solo else dur_c)[role].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
-    def pmc(kind):
-        f = next((src / kind).rglob("*counter_collection.csv"))
-        rows = [r for r in load_rows(f)]
+    def pmc(kind, counter=None):
+        """per role: the counter's value per dispatch (rows of other counters of a multi-counter
+        pass are dropped before the roles are assigned, so every dispatch appears once)"""
+        d = src / kind
+        if not d.exists():
+            return {}
+        f = next(d.rglob("*counter_collection.csv"))
+        rows = [r for r in load_rows(f) if counter is None or r.get("Counter_Name") == counter]
         rr = roles_by_queue(rows, key="Dispatch_Id")
         acc = defaultdict(list)
         for r, role in zip(rows, rr):
@@ -152,6 +157,12 @@ def main():
         return acc
 
     fetch, write = pmc("fetch"), pmc("write")
+    busy, gui = pmc("mfma", "SQ_VALU_MFMA_BUSY_CYCLES"), pmc("mfma", "GRBM_GUI_ACTIVE")
+    wcyc, wait = pmc("mfma", "SQ_WAVE_CYCLES"), pmc("mfma", "SQ_WAIT_ANY")
+    hit, miss = pmc("l2", "TCC_HIT_sum"), pmc("l2", "TCC_MISS_sum")
+
+    def mean(v):
+        return sum(v) / len(v) if v else float("nan")
     M, D = lane_b * 50, 768
     # (rows, N, K) of each GEMM role per launch; c_fc with the whole-round row split: the main
     # launch covers rows [0, m1), the tail launch the rest
@@ -170,9 +181,12 @@ def main():
              "times); concurrent us: the timed loop's dispatches, two lanes sharing the GPU. TFLOP/s = the",
              "launch's own FLOPs / isolated average. Algorithmic MB = A + W + C (16-bit) once. PMC MB =",
              "2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction; L2 misses served from the Infinity Cache are",
-             "counted, writes still dirty in L2 at kernel end are not).", "",
-             "| role | isolated dispatches | avg us | TFLOP/s | concurrent avg us | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic |",
-             "|---|---|---|---|---|---|---|---|---|"]
+             "counted, writes still dirty in L2 at kernel end are not). Counter passes (one rocprofv3 run",
+             "each, same command): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8",
+             "XCDs); MFMA busy x 2.5166 PF/s = the MFMA-issue rate the counters saw; wait = SQ_WAIT_ANY /",
+             "SQ_WAVE_CYCLES (wave-cycles parked on a counter or barrier); L2 hit = TCC_HIT / (HIT + MISS).", "",
+             "| role | isolated dispatches | avg us | TFLOP/s | frac of 2.5166 PF | concurrent avg us | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic | MFMA busy | wait | L2 hit |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     traffic = {}
     for role in sorted(set(dur) | set(dur_c), key=lambda k: -sum(dur.get(k, [])) - sum(dur_c.get(k, []))):
         d = dur.get(role) or dur_c[role]
@@ -180,20 +194,32 @@ def main():
         dc = dur_c.get(role, [])
         cavg = f"{sum(dc) / len(dc):.1f}" if dc else ""
         tf = f"{flops[role] / (avg * 1e-6) / 1e12:.0f}" if role in flops else ""
+        fr = f"{flops[role] / (avg * 1e-6) / 2.5166e15:.3f}" if role in flops else ""
+        mb = mean(busy.get(role, [])) / (1024 * mean(gui.get(role, [])) / 8) if busy.get(role) else float("nan")
+        wt = mean(wait.get(role, [])) / mean(wcyc.get(role, [])) if wait.get(role) else float("nan")
+        h, m_ = mean(hit.get(role, [])), mean(miss.get(role, []))
+        l2 = h / (h + m_) if hit.get(role) else float("nan")
         fb = 2 * sum(fetch[role]) / len(fetch[role]) * 1024 / 1e6 if fetch.get(role) else float("nan")
         wb = sum(write[role]) / len(write[role]) * 1024 / 1e6 if write.get(role) else float("nan")
-        traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6}
+        traffic[role] = {"avg_us": avg, "read_bytes": fb * 1e6, "write_bytes": wb * 1e6, "mfma_busy": mb,
+                         "wait_share": wt, "l2_hit": l2}
         al = f"{algo[role] / 1e6:.1f}" if role in algo else ""
         ratio = f"{(fb + wb) * 1e6 / algo[role]:.2f}" if role in algo else ""
-        lines.append(f"| {role} | {len(dur.get(role, []))} | {avg:.1f} | {tf} | {cavg} | {fb:.1f} | {wb:.1f} | {al} | {ratio} |")
+        lines.append(f"| {role} | {len(dur.get(role, []))} | {avg:.1f} | {tf} | {fr} | {cavg} | {fb:.1f} | {wb:.1f} | {al} | {ratio} "
+                     f"| {mb:.3f} | {wt:.3f} | {l2:.3f} |")
     if "fc_tail" in traffic:  # one c_fc invocation = main + tail launch
         a, b = traffic["fc"], traffic.pop("fc_tail")
-        traffic["fc"] = {k: a[k] + b[k] for k in a}
+        wa, wb_ = a["avg_us"], b["avg_us"]  # time-weighted counter shares
+        traffic["fc"] = {k: a[k] + b[k] for k in ("avg_us", "read_bytes", "write_bytes")}
+        for k in ("mfma_busy", "wait_share", "l2_hit"):
+            traffic["fc"][k] = (a[k] * wa + b[k] * wb_) / (wa + wb_)
         t = traffic["fc"]
         fl, al = flops["fc"] + flops["fc_tail"], algo["fc"] + algo["fc_tail"]
-        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | | "
+        lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
+                     f"{fl / (t['avg_us'] * 1e-6) / 2.5166e15:.3f} | | "
                      f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} | {al / 1e6:.1f} | "
-                     f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} |")
+                     f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} | {t['mfma_busy']:.3f} | {t['wait_share']:.3f} | "
+                     f"{t['l2_hit']:.3f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
     mlp = [traffic[r] for r in ("fc", "proj") if r in traffic]
     entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
@@ -201,9 +227,12 @@ def main():
              "note": "HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE reports half of wide streaming reads); Infinity-Cache hits are included by the counters"}
     if "fc" in traffic:  # bench.py --traffic-json: the dominant kernel's own PMC bytes per launch
         t = traffic["fc"]
+        fl = flops["fc"] + flops.get("fc_tail", 0)
         (prof / f"{tag}_fc_traffic.json").write_text(json.dumps({
             "fc_gemm_bytes_per_launch": t["read_bytes"] + t["write_bytes"], "fc_gemm_avg_us": t["avg_us"],
             "fc_gemm_algorithmic_bytes": algo["fc"] + algo.get("fc_tail", 0),
+            "fc_gemm_frac_rocprof": fl / (t["avg_us"] * 1e-6) / 2.5166e15,
+            "fc_gemm_mfma_busy": t["mfma_busy"], "fc_gemm_wait_share": t["wait_share"], "fc_gemm_l2_hit": t["l2_hit"],
             "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)"}, indent=1))
     pj = prof / "pmc_traffic.json"
     data = json.loads(pj.read_text()) if pj.exists() else {}
