@@ -539,7 +539,7 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
     const int v8 = h->var8[role];
-    if ((v8 == 3 || v8 == 4) && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
+    if (v8 == 3 && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
     if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, v8) != 0 &&
         launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, 0) != 0) {
         g_err = "gemm8: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -1060,9 +1060,9 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "attn_q8") ok = flag(h->attn_q8);
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
-    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62-64)
+    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || (m[0] >= 62 && m[0] <= 64));
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "split_xcd") ok = parse_int(v, h->split_xcd);
@@ -1521,8 +1521,8 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     int rc;
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
-    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 60 ||
-                        variant == 61 || variant == 62 || variant == 63 || variant == 64 || variant == 65;
+    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
+                        variant == 63 || variant == 65;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

@@ -797,9 +797,6 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
         case 8:   // 256x256, 8 waves: main launch of the c_fc round split
             if (a.N % 256) return -1;
             return launch_pipe<T, 256, 256, 2, 4, 2>(s, epi, a);
-        case 13:  // 128x128, 8 waves: c_fc (QuickGELU epilogue)
-            if (a.N % 128) return -1;
-            return launch_pipe<T, 128, 128, 4, 2, 2>(s, epi, a);
         case 22:  // 160x128, 4 waves, two workgroups per CU: patch embedding
             if (a.N % 128) return -1;
             return launch_pipe<T, 160, 128, 2, 2, 2>(s, epi, a);
@@ -826,7 +823,7 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (variant >= 60 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
+    if (variant >= 62 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);

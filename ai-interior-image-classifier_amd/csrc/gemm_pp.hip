@@ -1,4 +1,5 @@
-// Ping-pong MFMA GEMM: 256x256 tiles, 8 waves in two wave groups staggered by one barrier.
+// Ping-pong MFMA GEMM: 256x256 tiles, 8 waves in two wave groups staggered by one barrier,
+// persistent (one workgroup per CU; variants 62 / 63) and stream-K (65).
 //
 //   C[M, N] = A[M, K] @ W[N, K]^T + bias (16-bit C; QuickGELU for c_fc)
 //
@@ -27,255 +28,6 @@
 
 namespace clipvit {
 
-// v[i] += bias[i] for the lane's 16 contiguous features (bias staged in LDS)
-__device__ __forceinline__ void colv_add16(float (&v)[16], const float* bias) {
-    const float4* b4 = (const float4*)bias;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float4 bb = b4[i];
-        v[4 * i] += bb.x; v[4 * i + 1] += bb.y; v[4 * i + 2] += bb.z; v[4 * i + 3] += bb.w;
-    }
-}
-
-template <typename T, int EPI, int SM>
-__global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
-    typedef typename T::vec8 vec8;
-    constexpr int BM = 256, BN = 256;
-    constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;  // 64 KB per 64-deep k-tile
-    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + BN * 4];
-    float* const colv = (float*)(smem + 2 * STAGE);
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2, wc = wave & 3;
-    const int nN = a.N / BN;
-    int mt, nt;
-    if (!tile_of_block(blockIdx.x, (a.M + BM - 1) / BM, nN, a.xcd_n, mt, nt)) return;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const size_t ldb = (size_t)a.K * 2;
-    const int nk = a.K >> 6;  // even, >= 2 (launcher)
-
-    // ---- staging: group 0 fills A (32 pieces of 8 rows x 128 B), group 1 fills W. Part p (0..3)
-    // of a k-tile = pieces 8p + 2 wc + {0, 1} of the group's operand (one phase's issue).
-    const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
-    const int r0 = grp == 0 ? m0 : n0, rows = grp == 0 ? a.M : a.N;
-    const size_t opbytes = (size_t)(rows - r0) * ldb;
-    const i32x4_t rs = buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(opbytes < 0xFFFFFFFFu ? opbytes : 0xFFFFFFFFu));
-    const int lr = lane >> 3, chunk = (lane & 7) ^ lr;  // piece rows are 8-aligned: row & 7 = lr
-    unsigned voff[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
-        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);  // rows past M / N: out of range -> 0
-    }
-    const int opbase = grp == 0 ? 0 : A_BYTES;
-    auto issue = [&](int part, int j) {
-        if (j >= nk) return;
-        unsigned char* dst = smem + (j & 1) * STAGE + opbase;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int pc = 8 * part + 2 * wc + i;
-            blds16(rs, voff[2 * part + i], j * 128, dst + pc * 1024);
-        }
-    };
-
-    // epilogue bias: one column per thread, loaded now, parked in LDS at the end
-    float cb = 0.f;
-    if (tid < BN && a.bias) cb = a.bias[n0 + tid];
-
-    f32x4 acc[4][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // ---- prologue: k-tile 0 whole, then what the steady state issues before phase q0 of k-tile 0
-    // (group 0: part 0 of k-tile 1 at q3(-1); group 1: parts 0, 1 of k-tile 1 at q2(-1), q3(-1))
-#pragma unroll
-    for (int p = 0; p < 4; ++p) issue(p, 0);
-    if (grp == 0) {
-        issue(0, 1);
-        vm_wait<2>();
-    } else {
-        issue(0, 1);
-        issue(1, 1);
-        vm_wait<4>();
-    }
-    __builtin_amdgcn_s_barrier();
-    if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
-
-    const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
-    const int aoff = (grp * 128 + lrow) * 128, woff = A_BYTES + (wc * 64 + lrow) * 128;
-    const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;  // k-halves 0 / 1
-    vec8 af[4][2], wf[4][2];
-
-    // one k-tile (4 phases) on stage S
-    auto ktile = [&](const int kt, const unsigned char* st) {
-        // q0: A rows 0-63 of the wave's half, W features 0-31
-#pragma unroll
-        for (int f = 0; f < 2; ++f) {
-            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
-            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
-        }
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            af[f][0] = *(const vec8*)(st + aoff + f * 2048 + c0);
-            af[f][1] = *(const vec8*)(st + aoff + f * 2048 + c1);
-        }
-        if (grp == 0) issue(1, kt + 1); else issue(2, kt + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        // q1: W features 32-63 (last W read of this stage)
-#pragma unroll
-        for (int f = 2; f < 4; ++f) {
-            wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
-            wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
-        }
-        if (grp == 0) issue(2, kt + 1); else issue(3, kt + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int fn = 2; fn < 4; ++fn)
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        // q2: A rows 64-127 (last A read of this stage); W of k-tile kt + 2 may refill it now
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c0);
-            af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c1);
-        }
-        if (grp == 0) issue(3, kt + 1); else issue(0, kt + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int fn = 2; fn < 4; ++fn)
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm) acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm + 4]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        // q3: no reads (W features 0-31 still in registers); the A rows of group 0 may refill
-        if (grp == 0) {
-            issue(0, kt + 2);
-        } else {
-            issue(1, kt + 2);
-            // W of k-tile kt + 1 landed before group 0 reads it (next slot)
-            if (kt + 2 < nk) vm_wait<4>(); else vm_wait<0>();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-            for (int fn = 0; fn < 2; ++fn)
-#pragma unroll
-                for (int fm = 0; fm < 4; ++fm) acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], acc[fn][fm + 4]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (grp == 0) {  // A of k-tile kt + 1 landed before its first read
-            if (kt + 2 < nk) vm_wait<2>(); else vm_wait<0>();
-        }
-        __builtin_amdgcn_s_barrier();
-    };
-
-    for (int kt = 0; kt < nk; kt += 2) {
-        ktile(kt, smem);
-        ktile(kt + 1, smem + STAGE);
-    }
-    if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger: group 1's last MFMAs done
-
-    // ---- epilogue: bias (LDS), optional QuickGELU, 16-bit stores ----
-    constexpr bool GELU = EPI == EPI_GELU;
-    if (tid < BN) colv[tid] = cb;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    const int g = lg;
-    if constexpr (SM == 3) {
-        // row-contiguous stores staged through the (now free) LDS ring, as gemm.hip SM = 3
-        constexpr int ROWB = BN * 2, CPR = ROWB / 16;
-#pragma unroll
-        for (int fm = 0; fm < 8; ++fm) {
-            const int r = grp * 128 + fm * 16 + lrow;
-            const int nl = wc * 64 + 16 * g;
-            float v[16];
-#pragma unroll
-            for (int f = 0; f < 4; ++f)
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
-            colv_add16(v, colv + nl);
-            if constexpr (GELU) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
-            }
-            const int cc = nl >> 3;
-            unsigned char* rowp = smem + r * ROWB;
-            *(uint4*)(rowp + (((cc) ^ (r & 7)) << 4)) =
-                make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
-            *(uint4*)(rowp + (((cc + 1) ^ (r & 7)) << 4)) =
-                make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-        unsigned char* Cb = (unsigned char*)a.C;
-#pragma unroll 4
-        for (int i = tid; i < BM * CPR; i += 512) {
-            const int r = i / CPR, c = i % CPR;
-            const int m = m0 + r;
-            const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
-            if (m < a.M) *(uint4*)(Cb + ((size_t)m * a.ldc + n0) * 2 + c * 16) = val;
-        }
-    } else {
-        unsigned char* Cb = (unsigned char*)a.C;
-#pragma unroll
-        for (int fm = 0; fm < 8; ++fm) {
-            const int m = m0 + grp * 128 + fm * 16 + lrow;
-            if (m >= a.M) continue;
-            const int nl = wc * 64 + 16 * g;
-            float v[16];
-#pragma unroll
-            for (int f = 0; f < 4; ++f)
-#pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
-            colv_add16(v, colv + nl);
-            if constexpr (GELU) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
-            }
-            const size_t off = ((size_t)m * a.ldc + n0 + nl) * 2;
-            *(uint4*)(Cb + off) =
-                make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7]));
-            *(uint4*)(Cb + off + 16) =
-                make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15]));
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------
 // Persistent form (variant 62): one workgroup per CU walks the tiles blockIdx.x, blockIdx.x + G,
 // ... (G = grid size; logical ids through the same bijective XCD remap, so every XCD group
@@ -285,15 +37,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pp_kernel(GemmArgs a) {
 // (bias, QuickGELU, 16-bit stores straight from the accumulators) runs in the first read
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
-//
-// RC (variant 64): row-contiguous epilogue stores. From the accumulators a lane holds 32 B of one
-// token row, so a plain store instruction writes 16 B into each of 16 rows per quarter-wave: the
-// CU's store pipe then moves ~16 partial lines per 256 B and one CU's 128 KB tile takes ~3.7 us
-// to leave it even on an idle chip (tools/probes/store_probe.hip: 5.7 us with one tile per CU on
-// 8 CUs, 2.7 us for the same bytes as whole 128-B rows). RC bounces every 16-row slab of the
-// wave (2 KB) through a private LDS slot in the free end of the bias region (N <= 4096) and
-// stores 8 whole rows per instruction.
-template <typename T, int EPI, bool NT = false, bool RC = false>
+
+template <typename T, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -301,7 +46,6 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     constexpr int NBIAS = 8192;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 160 KB
     float* const colv = (float*)(smem + 2 * STAGE);
-    constexpr int RC_OFF = 2 * STAGE + NBIAS * 4 - 8 * 2048;  // RC slots: bias entries 4096.. (N <= 4096)
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -497,58 +241,6 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
         }
-        // RC: the wave's LDS slot (2 KB at the end of the LDS image) and its lane addresses:
-        // write row lrow, 16-B chunks 2 lg, 2 lg + 1; read row (lane >> 3) (+ 8), chunk lane & 7;
-        // chunk c of row r sits at c ^ (r & 7) (conflict-free both ways). Software-pipelined:
-        // slab fm's LDS round trip runs under slab fm + 1's epilogue arithmetic. A wave's LDS
-        // instructions execute in order, so the reads see the slab's writes, and the lgkmcnt(0)
-        // before a slab's stores retires its reads before the next slab overwrites the slot.
-        if constexpr (RC) {
-            const unsigned slot = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + RC_OFF) + wave * 2048;
-            const unsigned wa0 = slot + lrow * 128 + (((2 * lg) ^ lsw) << 4);
-            const unsigned wa1 = slot + lrow * 128 + (((2 * lg + 1) ^ lsw) << 4);
-            const unsigned ra = slot + (lane >> 3) * 128 + (((lane & 7) ^ ((lane >> 3) & 7)) << 4);
-            const int rr0 = m0 + grp * 128 + (lane >> 3);
-            const size_t cb = (size_t)(n0 + wc * 64 + 8 * (lane & 7)) * 2;
-            auto put = [&](int fm, const u32x4& o0, const u32x4& o1) {
-                const int mr = rr0 + fm * 16;
-                const size_t off = (size_t)mr * a.ldc * 2 + cb;
-#if CLIPVIT_ABLATE == 3  // diagnostic build only: no epilogue stores (values kept live)
-                if (a.ldc > (1 << 30)) {
-#else
-                {
-#endif
-                    if (mr < a.M) *(u32x4*)(Cb + off) = o0;
-                    if (mr + 8 < a.M) *(u32x4*)(Cb + off + (size_t)8 * a.ldc * 2) = o1;
-                }
-            };
-            u32x4 o0, o1;
-#pragma unroll
-            for (int fm = 0; fm < 8; ++fm) {
-                float v[16];
-#pragma unroll
-                for (int f = 0; f < 4; ++f)
-#pragma unroll
-                    for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
-                if constexpr (GELU) {
-#pragma unroll
-                    for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
-                }
-                const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
-                const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
-                                  pack2<T>(v[14], v[15])};
-                if (fm > 0) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    put(fm - 1, o0, o1);
-                }
-                asm volatile("ds_write_b128 %0, %1" ::"v"(wa0), "v"(w0) : "memory");
-                asm volatile("ds_write_b128 %0, %1" ::"v"(wa1), "v"(w1) : "memory");
-                asm volatile("ds_read_b128 %0, %1" : "=v"(o0) : "v"(ra) : "memory");
-                asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(o1) : "v"(ra) : "memory");
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            put(7, o0, o1);
-        } else {
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = m0 + grp * 128 + fm * 16 + lrow;
@@ -578,7 +270,6 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
                     *(u32x4*)(Cb + off + 16) = w1;
                 }
             }
-        }
         }
         if (!has_next) break;
         m0 = mn;
@@ -931,28 +622,16 @@ __global__ __launch_bounds__(512, 1) void gemm_psk_kernel(GemmArgs a, int ntiles
     if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 }
 
-template <typename T>
-static int launch_pp_t(hipStream_t s, int epi, const GemmArgs& a, int sm) {
-    const int nwg = grid_for((a.M + 255) / 256, a.N / 256, a.xcd_n);
-#define PP(E, S) gemm_pp_kernel<T, E, S><<<nwg, 512, 0, s>>>(a)
-    if (epi == EPI_STORE) { if (sm == 3) PP(EPI_STORE, 3); else PP(EPI_STORE, 0); return 0; }
-    if (epi == EPI_GELU) { if (sm == 3) PP(EPI_GELU, 3); else PP(EPI_GELU, 0); return 0; }
-#undef PP
-    return -1;
-}
-
-template <typename T, bool NT, bool RC>
+template <typename T, bool NT>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, RC><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, RC><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
-// variant 60: direct stores from the accumulators; 61: LDS-staged row-contiguous stores;
-// 62: persistent (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with non-temporal stores
 template <typename T>
 static int launch_psk_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
@@ -962,26 +641,22 @@ static int launch_psk_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int grid = ncu;
     // every share must cover at least one tile's k-tiles (EARLY and LATE then lie in different
     // tiles, and a tile is split between at most two workgroups)
-    if (I / grid < nk || !a.sk_part || !a.sk_flag) return launch_ppp_t<T, false, false>(s, epi, a);  // whole tiles
+    if (I / grid < nk || !a.sk_part || !a.sk_flag) return launch_ppp_t<T, false>(s, epi, a);  // whole tiles
     if (epi == EPI_STORE) { gemm_psk_kernel<T, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     if (epi == EPI_GELU) { gemm_psk_kernel<T, EPI_GELU><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
+// variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
+// non-temporal stores; 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
+// would be shorter than one tile's k-tiles)
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
-    if (variant == 65) {  // stream-K (workspace in a.sk_part / a.sk_flag)
-        if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-        return dtype == 2 ? launch_psk_t<F16>(s, epi, a) : launch_psk_t<BF16>(s, epi, a);
-    }
-    if (variant >= 62 && variant <= 64) {
-        if (a.N > (variant == 64 ? 4096 : 8192) || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-        if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true, false>(s, epi, a) : launch_ppp_t<BF16, true, false>(s, epi, a);
-        if (variant == 64) return dtype == 2 ? launch_ppp_t<F16, false, true>(s, epi, a) : launch_ppp_t<BF16, false, true>(s, epi, a);
-        return dtype == 2 ? launch_ppp_t<F16, false, false>(s, epi, a) : launch_ppp_t<BF16, false, false>(s, epi, a);
-    }
-    const int sm = variant == 61 ? 3 : 0;
-    return dtype == 2 ? launch_pp_t<F16>(s, epi, a, sm) : launch_pp_t<BF16>(s, epi, a, sm);
+    if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
+    if (variant == 65) return dtype == 2 ? launch_psk_t<F16>(s, epi, a) : launch_psk_t<BF16>(s, epi, a);
+    if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
+    if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
+    return -1;
 }
 
 }  // namespace clipvit

@@ -413,7 +413,7 @@ static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Ping-pong MX-fp8 tile (variants 3 persistent / 4 one tile per workgroup): gemm_ppp_kernel's
+// Ping-pong MX-fp8 tile (variant 3, persistent): gemm_ppp_kernel's
 // schedule (gemm_pp.hip) at BK = 128 fp8. A k-tile row is 128 B in both
 // formats, so the LDS layout, the staging pieces and the phase/slot plan are the 16-bit
 // kernel's; per phase a wave runs 8 scaled 16x16x128 MFMAs (2x the cycles of the 16-bit form,
@@ -733,7 +733,7 @@ static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persist
 }
 
 // variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves), 3 ping-pong 256x256
-// persistent, 4 ping-pong 256x256 one tile per workgroup, 5 160x128 (2x2 waves; two per CU,
+// persistent, 5 160x128 (2x2 waves; two per CU,
 // 480 tiles = one round at M = 12,800, N = 768)
 template <typename TO>
 static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
@@ -742,7 +742,6 @@ static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) 
         case 1: return launch_mx8_tile<TO, 128, 256, 2, 4>(s, epi, a);
         case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
         case 3: return launch_mx8_pp<TO>(s, epi, a, true);
-        case 4: return launch_mx8_pp<TO>(s, epi, a, false);
         case 5: return launch_mx8_tile<TO, 160, 128, 2, 2>(s, epi, a);
     }
     return -1;

@@ -109,11 +109,11 @@ def test_gemm_mx8_vs_dequantized_reference(gpu, variant, M, N, K):
     assert err < 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [3, 4, 5])
+@pytest.mark.parametrize("variant", [3, 5])
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
                                    (700, 768, 3072), (257, 512, 256)])
 def test_gemm_mx8_ping_pong_bit_identical(gpu, variant, M, N, K):
-    """The 256x256 ping-pong MX tile (3 persistent, 4 one tile per workgroup) and the 160x128
+    """The persistent 256x256 ping-pong MX tile (3) and the 160x128
     tile (5, two scale dwords per thread) accumulate every output in the same k order as the
     128x256 tile: their bf16 store and MX-fp8 (QuickGELU) output must be bit-identical to
     variant 1's, over repeated launches (race screen, as test_gpu_kernels.py's ping-pong

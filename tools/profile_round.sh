@@ -7,6 +7,8 @@
 #                                            -> MFMA busy, clock, wait share per dispatch (own pass)
 #   5. rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -> L2 hit rate per dispatch (own pass)
 #   6. tools/summarize_profiles.py (host only) -> profiles/<tag>_summary.md, <tag>_fc_traffic.json
+#      (written on the box for step 7; only gpurun_out/ comes back: re-run it here on the merged
+#      gpurun_out/prof to commit them)
 #   7. the default bench once more, with --traffic-json of step 6 -> $OUT/bench_traffic.json
 # Usage: bash tools/profile_round.sh OUTDIR TAG
 set -e

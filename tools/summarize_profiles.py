@@ -233,7 +233,7 @@ def main():
             "fc_gemm_algorithmic_bytes": algo["fc"] + algo.get("fc_tail", 0),
             "fc_gemm_frac_rocprof": fl / (t["avg_us"] * 1e-6) / 2.5166e15,
             "fc_gemm_mfma_busy": t["mfma_busy"], "fc_gemm_wait_share": t["wait_share"], "fc_gemm_l2_hit": t["l2_hit"],
-            "source": f"profiles/{tag}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py)"}, indent=1))
+            "source": f"profiles/{tag}_summary.md (rocprofv3 kernel trace + --pmc FETCH_SIZE / WRITE_SIZE / MFMA-busy / L2 passes of bench.py)"}, indent=1))
     pj = prof / "pmc_traffic.json"
     data = json.loads(pj.read_text()) if pj.exists() else {}
     entry["images_per_launch"] = lane_b
