@@ -100,7 +100,7 @@ constexpr int kLanes = 2;
 // faster one; bf16 bs 512 81.5k -> 86.8k and 84.1k -> 87.0k; MX-fp8 bs 512 93.0k -> 99.0k;
 // L/14@336 bs 128 2,183 -> 2,269 and 2,179 -> 2,280; B/16 bs 256 21.25k -> 21.43k. Smaller
 // batches lose (B/32 bs 64 39.4k -> 38.2k, B/16 bs 64 20.3k -> 19.6k). Round 1 measured a loss
-// at bs 256 with the earlier tile table. CLIPVIT_SPLIT_MIN=n overrides (<= 0: never split).
+// at bs 256 with the earlier tile table. tuning split_min=n overrides (<= 0: never split).
 constexpr int SPLIT_NEVER = 1 << 30;
 constexpr int SPLIT_TOKENS = 25600, SPLIT_IMAGES = 128;
 struct Workspace {
@@ -151,7 +151,7 @@ struct clipvit_handle {
     std::mutex mu;
     std::vector<Workspace*> pool;
     // GEMM tile variants per role (qkv, out, fc, proj, patch), from in-model sweeps on MI355X
-    // (tools/ab_env.sh); overridable with CLIPVIT_GEMM_VARIANTS="q,o,f,p,e".
+    // (profiles/ablog.md; tools/ab_envs.sh); tuning gemm_variants="q,o,f,p,e".
     // 22 = 160x128 tiles of 4 waves, two workgroups per CU (the N = 768 roles). The 224x192
     // one-round tiles 92 / 93 win standalone (c_proj 67.4 -> 62.7 us, patch 75.2 -> 69.6) but
     // not in-model (c_proj 0.777 -> 0.785-0.81 ms per forward, patch 0.134 -> 0.143-0.158).
@@ -161,16 +161,16 @@ struct clipvit_handle {
     // 0.795 ms per forward as with the round split (8 + 81), c_proj after it 0.675 -> 0.658 ms,
     // B/32 bs 256 85.6k -> 86.3k img/s (2 same-box alternations)
     int var[5] = {98, 82, 22, 82, 22};
-    bool var_forced = false;  // CLIPVIT_GEMM_VARIANTS given: no shape-based override
+    bool var_forced = false;  // tuning gemm_variants given: no shape-based override
     // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
     // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
     // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
     // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
-    // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). CLIPVIT_LARGE_VARIANTS="q,f[,o,p]"
+    // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). tuning large_variants="q,f,o,p"
     int large_var[4] = {3462, 3463, 3463, 3463};  // QKV, c_fc, out_proj, c_proj
     int ncu = 256;            // compute units of the device
-    // tile->XCD partition per role (CLIPVIT_GEMM_XCD="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
+    // tile->XCD partition per role (tuning gemm_xcd="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
     // (c_proj 69.9 vs 70.0 us, out 24.0 vs 24.1) with each A panel read by one XCD instead of
     // two: PMC bytes / algorithmic 1.61 -> 1.13 (c_proj) and 1.33 -> 1.02 (out_proj)
@@ -180,7 +180,7 @@ struct clipvit_handle {
     // MX-fp8 GEMMs (packed weight = N*Kp e4m3 bytes followed by N*Kp/32 E8M0 scales);
     // patch embedding, attention and everything else stay bf16 / fp32.
     bool mx8 = false;
-    // MX-fp8 GEMM tile per role (qkv, out, fc, proj); CLIPVIT_MX8_VARIANTS. 128x128 everywhere:
+    // MX-fp8 GEMM tile per role (qkv, out, fc, proj); tuning mx8_variants. 128x128 everywhere:
     // measured at M = 25,600 (bs 512) qkv 88 -> 80 us, c_fc 110 -> 103 us against 128x256
     // out_proj on 160x128 (5): 480 tiles = one round at two per CU where 128x128 needs 1.17
     // (M = 12,800: 18.2 -> 15.1 us standalone, config 5 +1.7-2.3 % same box). c_fc on the
@@ -189,43 +189,41 @@ struct clipvit_handle {
     int var8[4] = {3, 5, 3, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
-    // four in bf16 — DESIGN.md §MX-fp8); CLIPVIT_MX8_SKIP="..." overrides ("" = none)
+    // four in bf16 — DESIGN.md §MX-fp8); tuning mx8_skip="..." overrides
     uint64_t mx8_skip = 0;
     // blocks whose MLP (c_fc, c_proj) stays bf16: the attention roles (QKV, out_proj) follow
-    // mx8_skip, the MLP roles this mask (CLIPVIT_MX8_SKIP sets both, CLIPVIT_MX8_SKIP_MLP this one):
+    // mx8_skip, the MLP roles this mask (tuning mx8_skip sets both, mx8_skip_mlp this one):
     // the MLP GEMMs carry most of the MX-fp8 error, QKV / out_proj little of it
     uint64_t mx8_skip_mlp = 0;
     bool q8_attn(int i) const { return mx8 && !((mx8_skip >> i) & 1); }
     bool q8_mlp(int i) const { return mx8 && !((mx8_skip_mlp >> i) & 1); }
     // residual adds of out_proj / c_proj: true = the GEMM stores its 16-bit branch output y and
-    // the following LayerNorm kernel does x += y (fp16 and bf16 default; CLIPVIT_RESID16=0/1 overrides);
+    // the following LayerNorm kernel does x += y (fp16 and bf16 default, set in clipvit_create; tuning resid16);
     // false = fp32 read-modify-write of x in the GEMM epilogue
     bool resid16 = false;
-    // deferred residual store (fp16 path, see forward()); CLIPVIT_DEFER_X=0 disables
+    // deferred residual store (fp16 path, see forward()); tuning defer_x=0 disables
     bool defer_x = true;
-    // LayerNorm fold (CLIPVIT_LNFOLD=1, fp16 only): ln_1 / ln_2
+    // LayerNorm fold (tuning lnfold=1, fp16 only): ln_1 / ln_2
     // become per-row statistics written by the residual producers' epilogues (out_proj, c_proj,
     // embedding) and an affine correction in the QKV / c_fc epilogues; no LayerNorm pass
     bool lnfold = false;
     float* scratch2 = nullptr;  // W diag(gamma) staging for the folded Linears
-    // last block on class-token rows only (see cls_tail); CLIPVIT_CLS_PRUNE=0 disables
+    // last block on class-token rows only (see cls_tail); tuning cls_prune=0 disables
     bool cls_prune = true;
     unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
-    int max_inflight = 2;  // workspaces kept for calls in flight on different streams (CLIPVIT_MAX_INFLIGHT)
-    int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; CLIPVIT_TAIL_VARIANT)
-    // whole-round row split of the 16-bit-output GEMMs (see gemm()); off by default since c_fc
-    // runs on the 160x128 tile (var above); CLIPVIT_GEMM_SPLIT=1 enables
+    int max_inflight = 2;  // workspaces kept for calls in flight on different streams (tuning max_inflight)
+    int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; tuning tail_variant)
     // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
     // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
     // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
     // MX-fp8 forward, fp16 residual stream: the residual x lives in fp16 between the LayerNorm
     // kernels (which add and normalise in fp32) instead of fp32, halving their x bytes
     // (LayerNorm family = 30 % fewer HBM bytes). Needs the deferred 16-bit branch path and a
-    // 16-bit class-token tail (the tail widens the class rows to fp32). CLIPVIT_X16=0: fp32 x.
+    // 16-bit class-token tail (the tail widens the class rows to fp32). tuning x16=0: fp32 x.
     bool x16 = true;
     // 16-bit forward (fp16 / bf16), 24-bit residual stream: x between the LayerNorm kernels as
     // 16 + 8 bit planes (norm.hip x24_load) instead of fp32: the add + LayerNorm kernels move 3
-    // bytes per element of x instead of 4 (CLIPVIT_X24=0: fp32 x)
+    // bytes per element of x instead of 4 (tuning x24=0: fp32 x)
     bool x24 = true;
     bool use_x24() const { return x24 && !mx8 && !lnfold && resid16 && defer_x && cls_prune; }
     bool use_x16() const {
@@ -233,11 +231,11 @@ struct clipvit_handle {
                ((mx8_skip_mlp >> (cfg.layers - 1)) & 1);
     }
     // MX-fp8 forward: attention writes the out_proj operand (MX-fp8) itself instead of 16-bit
-    // output + launch_quant_mx8 (same bytes; CLIPVIT_ATTN_Q8=0 restores the two kernels)
+    // output + launch_quant_mx8 (same bytes; tuning attn_q8=0 restores the two kernels)
     bool attn_q8 = true;
     bool round_split = true;
-    int split_main = 62, split_tail = 81;  // tiles of the two launches (0 = the role's); CLIPVIT_SPLIT_VARIANTS="m,t"
-    // XCD map of the main launch (tile_of_block; CLIPVIT_SPLIT_XCD): 34 = the 1-D remap over a
+    int split_main = 62, split_tail = 81;  // tiles of the two launches (0 = the role's); tuning split_variants
+    // XCD map of the main launch (tile_of_block; tuning split_xcd): 34 = the 1-D remap over a
     // column-group-major order with 2 N-groups, so each XCD group keeps half of W (2.4 MB of
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
     // ms per forward, main-launch traffic 1.59x -> 1.38x of algorithmic
@@ -249,6 +247,10 @@ struct clipvit_handle {
     // panel need its k-slices at different times and the L2 working set becomes whole panels
     // (2.5 us per k-tile against 1.7)
     unsigned sk_roles = 0;
+    // c_fc -> c_proj intermediate u in the 16-row blocked layout (common.h blk16_off): c_fc's
+    // accumulator-layout stores become 256-B runs per quarter-wave instead of 16 scattered
+    // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
+    bool u_blk = true;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -313,7 +315,7 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
     hipError_t e = hipEventCreateWithFlags(&w->fork, hipEventDisableTiming);
     for (auto& l : w->lane) {
         l.cap = lane_cap(h);
-        const size_t rows = (size_t)l.cap * h->N;
+        const size_t rows = ((size_t)l.cap * h->N + 15) / 16 * 16;  // u: whole 16-row blocks
         const size_t R = h->cfg.image_size;
         const size_t Rw = (R / h->cfg.patch_size) * ((h->cfg.patch_size + 7) / 8 * 8);  // padded pixel rows
         const size_t ubytes = std::max(rows * 4 * h->D * 2, (size_t)l.cap * 3 * R * Rw * 2);
@@ -422,6 +424,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
+    a.blk_c = h->u_blk && role == R_FC;  // every R_FC output / R_PROJ input is the lane's u
+    a.blk_a = h->u_blk && role == R_PROJ;
     int variant = h->var[role];
     // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
     // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
@@ -1060,6 +1064,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "attn_q8") ok = flag(h->attn_q8);
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
+    else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63)
         int m[2] = {h->split_main, h->split_tail};
         ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
@@ -1110,7 +1115,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
         int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
@@ -1118,7 +1123,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
+              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
               g->split_min, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
@@ -1132,7 +1137,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
         if (rc) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
-            h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced;
+            h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
             memcpy(h->xcd, before.xcd, sizeof before.xcd);
@@ -1519,7 +1524,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         a.sk_epoch = 1;
     }
     int rc;
-    // 16-bit-output-only variants (80-82, 98 LDS-staged; 60 / 61 ping-pong), or epi 10 / 11 = 16-bit STORE / GELU on
+    // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 / 65 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
                         variant == 63 || variant == 65;

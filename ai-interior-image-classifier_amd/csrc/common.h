@@ -179,7 +179,21 @@ struct GemmArgs {
     unsigned* sk_flag;
     unsigned sk_epoch;
     unsigned long long* sk_trace;  // diagnostic (bench entry only): per-workgroup s_memrealtime stamps
+    // 16-row blocked layout (blk16_off) of the 16-bit A operand / C output: c_fc -> c_proj's u.
+    // Pipelined (gemm_pipe_kernel) and persistent ping-pong (62 / 63) kernels only; the others
+    // refuse it. Rows are padded to a multiple of 16 in the buffer.
+    int blk_a, blk_c;
 };
+
+// 16-row blocked layout of a 16-bit [rows, ncols] matrix (ncols % 64 == 0): 16 x 64 blocks of
+// 2 KB, row-block-major; inside a block the eight 16-B feature chunks are stored chunk-major,
+// 16 rows each. One 16-B column of 16 consecutive rows (what a quarter-wave of the MFMA
+// accumulator layout holds) is then 256 contiguous bytes, and a 64-deep k-tile of a 16-row
+// block is one contiguous 2 KB run (the consumer's LDS image verbatim). Byte offset of (m, f):
+__host__ __device__ inline size_t blk16_off(int m, int f, int ncols) {
+    return ((((size_t)(m >> 4) * (size_t)(ncols >> 6)) + (size_t)(f >> 6)) << 11) + (size_t)(((f & 63) >> 3) << 8) +
+           (size_t)((m & 15) << 4) + (size_t)((f & 7) << 1);
+}
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
 // fixed order); eps 1e-5 as CLIP's LayerNorm

@@ -405,6 +405,18 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
 #pragma unroll
             for (int r = 0; r < LA; ++r)
                 boa[r] = (unsigned)(asrc[r] - b0 * img + 2 * ((acol[r] / CPR) * a.patch_Rw + 8 * (acol[r] % CPR)));
+        } else if (a.blk_a) {
+            // 16-row blocked A (blk16_off): the stage's LDS image is chunk-major per 16-row block,
+            // i.e. each block's 2 KB k-tile run copied verbatim (row blocks past the last one
+            // clamped; rows past M inside it are padding and only feed unstored output rows)
+            const int mpad = (a.M + 15) & ~15, lastb = (mpad - m0) / 16 - 1;
+            const size_t abytes = (size_t)(mpad - m0) * ldb;
+            rsA = buf_rsrc(Ab + (size_t)m0 * ldb, (unsigned)min(abytes, (size_t)0xFFFFFFFFu));
+#pragma unroll
+            for (int r = 0; r < LA; ++r) {
+                const int p = r * NT * 16 + tid * 16;
+                boa[r] = (unsigned)((size_t)min(p >> 11, lastb) * 16 * ldb + (p & 2047));
+            }
         } else {
             const size_t abytes = (size_t)(a.M - m0) * ldb;
             rsA = buf_rsrc(Ab + (size_t)m0 * ldb, (unsigned)min(abytes, (size_t)0xFFFFFFFFu));
@@ -420,7 +432,7 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         return;
 #endif
         if constexpr (BUFL) {
-            int aofs = (int)kofs;
+            int aofs = a.blk_a ? kt * 2048 : (int)kofs;  // (blk_a: no split-K, launch_pipe)
             if constexpr (PSEP) {  // channel kt / KPC, first pixel row (kt % KPC) * (64 / P)
                 constexpr int KPC = PIMPL * PIMPL / 64;
                 aofs = ((kt / KPC) * a.patch_R + (kt % KPC) * (64 / PIMPL)) * a.patch_Rw * 2;
@@ -445,12 +457,17 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     };
 
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
-    const int aoff = (wm * TM + lrow) * 128, woff = A_BYTES + (wn * TN + lrow) * 128;
+    // A fragment of row lrow, k-chunk (s << 2) | lg: swizzled row-major image, or (blk_a) the
+    // chunk-major image of the 16-row blocks (chunk * 256 + row * 16, conflict-free unswizzled)
+    const bool ablk = a.blk_a != 0;
+    const int aoff = ablk ? wm * TM * 128 + lrow * 16 : (wm * TM + lrow) * 128;
+    const int woff = A_BYTES + (wn * TN + lrow) * 128;
     auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
         const unsigned char* base = smem + buf * STAGE;
         const int c = (((s << 2) | lg) ^ lsw) << 4;
+        const int ca = ablk ? ((s << 2) | lg) << 8 : c;
 #pragma unroll
-        for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + c);
+        for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + ca);
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + c);
     };
@@ -615,6 +632,16 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
         unsigned char* Cb = (unsigned char*)a.C;
+        if (a.blk_c) {  // blocked C: a quarter-wave stores one chunk of 16 rows (256 B contiguous)
+#pragma unroll 4
+            for (int i = tid; i < BM * CPR; i += NT) {
+                const int r = ((i >> 4) / CPR) * 16 + (i & 15), c = (i >> 4) % CPR;
+                const int m = m0 + r;
+                const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
+                if (m < a.M) *(uint4*)(Cb + blk16_off(m, n0 + 8 * c, a.ldc)) = val;
+            }
+            return;
+        }
 #pragma unroll 4
         for (int i = tid; i < BM * CPR; i += NT) {
             const int r = i / CPR, c = i % CPR;
@@ -667,10 +694,12 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                 for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || LNF) {
-                const size_t off = ((size_t)m * a.ldc + n) * 2;
+                // blocked C: n % 16 == 0, so n + 8 is the next chunk of the same 64-block (+256 B)
+                const size_t off = a.blk_c ? blk16_off(m, n, a.ldc) : ((size_t)m * a.ldc + n) * 2;
+                const size_t off2 = a.blk_c ? off + 256 : off + 16;
                 *(uint4*)(Cb + off) = (make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
                                        pack2<T>(v[6], v[7])));
-                *(uint4*)(Cb + off + 16) = (make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                *(uint4*)(Cb + off2) = (make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
                                             pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
             } else if constexpr (EPI == EPI_RESID) {
                 const float4* src = (const float4*)((float*)a.C + (size_t)m * a.ldc + n);
@@ -823,6 +852,11 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
+    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 only
+        if (variant < 8 || variant == 65 || a.ksplit > 1) return -1;
+        if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
+            return -1;
+    }
     if (variant >= 62 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

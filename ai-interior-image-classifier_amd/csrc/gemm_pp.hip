@@ -65,7 +65,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         return true;
     };
     const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
-    const int rows = grp == 0 ? a.M : a.N;
+    // blocked A (blk_a, blk16_off; rows padded to 16): piece pc of the A stage is half pc & 1 of
+    // 16-row block pc >> 1, whose k-tile run is contiguous — the LDS image is chunk-major
+    const bool ablk = grp == 0 && a.blk_a;
+    const int rows = grp == 0 ? (a.blk_a ? (a.M + 15) & ~15 : a.M) : a.N;
     auto rsrc_of = [&](int m0, int n0) {
         const int r0 = grp == 0 ? m0 : n0;
         const size_t bytes = (size_t)(rows - r0) * ldb;
@@ -76,8 +79,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
-        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
+        voff[i] = ablk ? (unsigned)((pc >> 1) * 16 * ldb + (pc & 1) * 1024 + lane * 16)
+                       : (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
     }
+    const int kstride = ablk ? 2048 : 128;  // bytes per k-tile along a row (block)
     const int opbase = grp == 0 ? 0 : A_BYTES;
 
     int m0, n0, mn = 0, nn = 0;
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         }
         unsigned char* dst = smem + (j & 1) * STAGE + opbase;  // nk even: the stream's parity
 #pragma unroll
-        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * 128, dst + (8 * part + 2 * wc + i) * 1024);
+        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * kstride, dst + (8 * part + 2 * wc + i) * 1024);
     };
 
     f32x4 acc[4][8];
@@ -117,8 +122,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
-    const int aoff = (grp * 128 + lrow) * 128, woff = A_BYTES + (wc * 64 + lrow) * 128;
+    const int woff = A_BYTES + (wc * 64 + lrow) * 128;
     const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;
+    // A fragments: swizzled row-major image, or (blk_a) chunk-major 16-row blocks
+    const int aoff = a.blk_a ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
+    const int a0 = a.blk_a ? lg << 8 : c0, a1 = a.blk_a ? (4 | lg) << 8 : c1;
     vec8 af[4][2], wf[4][2];
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 
@@ -133,8 +141,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            af[f][0] = *(const vec8*)(st + aoff + f * 2048 + c0);
-            af[f][1] = *(const vec8*)(st + aoff + f * 2048 + c1);
+            af[f][0] = *(const vec8*)(st + aoff + f * 2048 + a0);
+            af[f][1] = *(const vec8*)(st + aoff + f * 2048 + a1);
         }
         if (grp == 0) issue(1, kt + 1); else issue(2, kt + 1);
         __builtin_amdgcn_sched_barrier(0);
@@ -175,8 +183,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         __builtin_amdgcn_s_barrier();
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c0);
-            af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + c1);
+            af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a0);
+            af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a1);
         }
         if (grp == 0) issue(3, kt + 1); else issue(0, kt + 2);
         __builtin_amdgcn_sched_barrier(0);
@@ -258,16 +266,18 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
 #else
             if (m < a.M) {
 #endif
-                const size_t off = ((size_t)m * a.ldc + n) * 2;
+                // blocked C (blk_c): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes
+                const size_t off = a.blk_c ? blk16_off(m, n, a.ldc) : ((size_t)m * a.ldc + n) * 2;
+                const size_t off2 = a.blk_c ? off + 256 : off + 16;
                 const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
                 const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
                                   pack2<T>(v[14], v[15])};
                 if constexpr (NT) {  // non-temporal: no L2 allocation for the output (A/B, §5.8)
                     __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
-                    __builtin_nontemporal_store(w1, (u32x4*)(Cb + off + 16));
+                    __builtin_nontemporal_store(w1, (u32x4*)(Cb + off2));
                 } else {
                     *(u32x4*)(Cb + off) = w0;
-                    *(u32x4*)(Cb + off + 16) = w1;
+                    *(u32x4*)(Cb + off2) = w1;
                 }
             }
         }

@@ -114,12 +114,13 @@ struct clipvit_text_handle {
     float *x = nullptr, *eot = nullptr, *f = nullptr;
     void *h = nullptr, *qkv = nullptr, *u = nullptr;
     hipEvent_t done = nullptr;
-    // GEMM tiles (qkv, out, fc, proj; CLIPVIT_TEXT_VARIANTS="q,o,f,p") and the fp16 residual
+    // GEMM tiles (qkv, out, fc, proj) and the fp16 residual
     // scheme of the vision tower (16-bit branch outputs + add_layernorm, deferred x store).
     // Measured on the 437 label prompts (M = 33,649): fc on 128x128 (v13) 4.84 ms per call
     // against 4.88-4.90 on 256x256 (v8: 1,056 tiles = 4.1 rounds); qkv 240x256 / 160x128 no
     // better than 256x256; resid16 4.89 against 5.00 ms with the fp32 epilogue adds
-    int var[4] = {80, 82, 13, 82};
+    // (fc: the 128x128 tile 81 since the direct-store 128x128 tile 13 was retired in r04)
+    int var[4] = {80, 82, 81, 82};
     bool resid16 = false;
 };
 
@@ -355,7 +356,7 @@ int clipvit_encode_text(clipvit_text_handle* h, void* stream, const int32_t* tok
     // resid16: out_proj / c_proj store their 16-bit branch outputs y, y2 into the qkv buffer (dead
     // once attention has read it) and add_layernorm does the residual adds, x stored once per
     // block ((x + y) + y2, the vision tower's deferred scheme, clipvit.hip forward()); the last
-    // block's c_proj adds into x in its epilogue (the EOT gather reads x). CLIPVIT_TEXT_RESID16=0:
+    // block's c_proj adds into x in its epilogue (the EOT gather reads x). resid16 = false:
     // fp32 residual read-modify-write in the GEMM epilogues.
     void* y = h->qkv;
     void* y2 = (u16*)h->qkv + (size_t)M * D;

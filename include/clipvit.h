@@ -96,7 +96,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
 /* Test / A-B hook, not part of the reference's surface: select one of the measured
  * alternatives DESIGN.md records instead of the shipped default, before clipvit_load_weights
  * (CLIPVIT_E_STATE after it). spec = "key=value;key=value", keys: resid16, defer_x, lnfold,
- * cls_prune, round_split, attn_q8, x16, x24 (0/1); split_variants "main,tail"; tail_variant;
+ * cls_prune, round_split, attn_q8, x16, x24, u_blocked (0/1); stream_k (role bit mask);
+ * split_variants "main,tail"; tail_variant;
  * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p"; mx8_skip / mx8_skip_mlp "i,j,.." (bf16
  * blocks; mx8_skip sets both masks). An unknown key or bad value fails with CLIPVIT_E_INVALID

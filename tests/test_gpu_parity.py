@@ -359,3 +359,36 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu):
         print(f"B/32 bs 256 lnfold: max rel logit err {rel:.2e}")
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("name,dtype,B,tun", [
+    ("ViT-B/32", "fp16", 256, {}),              # c_fc: ping-pong v62 main + v81 tail; c_proj v82
+    ("ViT-B/32", "bf16", 67, {}),               # one launch per role
+    ("ViT-B/32", "fp16", 1, {}),                # M = 50: the last 16-row block is padding
+    ("ViT-B/32", "fp16", 256, {"lnfold": 1}),   # EPI_LNF_GELU c_fc, EPI_RES_STATS c_proj
+    ("ViT-B/32", "fp16", 256, {"split_variants": "63,81"}),  # non-temporal ping-pong main
+    ("ViT-B/16", "fp16", 64, {}),               # N = 197, round split
+    ("ViT-L/14@336px", "fp16", 32, {}),         # large M: persistent v63 writes and reads u
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3463,80"}),  # v8 direct stores, v80 reads
+    ("ViT-B/32", "mxfp8", 64, {}),              # the 16-bit blocks of the MX-fp8 forward
+])
+def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
+    """The c_fc -> c_proj intermediate in the 16-row blocked layout (default; tuning u_blocked=0:
+    row-major) moves bytes only: every kernel computes the same values in the same order, so the
+    features equal the row-major run's bit for bit on every GEMM path that writes or reads u."""
+    cfg = C.get_config(name)
+    sd = synthetic_state_dict(cfg, 0)
+    ad = synthetic_adapters(cfg, rank=8)
+    px = _pixels(B, cfg.image_size, seed=47).to(gpu)
+    outs = []
+    for blk in (1, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, u_blocked=blk))
+        try:
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
