@@ -536,10 +536,16 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
                  const void* Wq, const float* bias, void* C, int M, int N, int K, int ldc,
                  int role) {
     GemmArgs a{};
-    a.A = A8; a.sA = A8 + (size_t)M * K;
+    // u8 (c_fc -> c_proj) in the 16-row blocked layout (blk8_off): its scales follow the padded
+    // rows, since the last block's real rows spread over the whole block
+    a.blk_c = h->u_blk && role == R_FC;
+    a.blk_a = h->u_blk && role == R_PROJ;
+    const size_t ma = a.blk_a ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
+    const size_t mc = a.blk_c ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
+    a.A = A8; a.sA = A8 + ma * K;
     a.W = Wq; a.sW = (const unsigned char*)Wq + (size_t)N * K;
     a.bias = bias; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = ldc;
-    if (epi == EPI_GELU_Q8) a.sC = (unsigned char*)C + (size_t)M * N;
+    if (epi == EPI_GELU_Q8) a.sC = (unsigned char*)C + mc * N;
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
     const int v8 = h->var8[role];

@@ -194,6 +194,13 @@ __host__ __device__ inline size_t blk16_off(int m, int f, int ncols) {
     return ((((size_t)(m >> 4) * (size_t)(ncols >> 6)) + (size_t)(f >> 6)) << 11) + (size_t)(((f & 63) >> 3) << 8) +
            (size_t)((m & 15) << 4) + (size_t)((f & 7) << 1);
 }
+// The same for a 1-byte (MX-fp8 e4m3) matrix, ncols % 128 == 0: 16 x 128 blocks of 2 KB, eight
+// 16-byte feature chunks per block, chunk-major (the MX GEMM's 128-deep k-tile of a 16-row block
+// is one contiguous 2 KB run). Byte offset of (m, f):
+__host__ __device__ inline size_t blk8_off(int m, int f, int ncols) {
+    return ((((size_t)(m >> 4) * (size_t)(ncols >> 7)) + (size_t)(f >> 7)) << 11) + (size_t)(((f & 127) >> 4) << 8) +
+           (size_t)((m & 15) << 4) + (size_t)(f & 15);
+}
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
 // fixed order); eps 1e-5 as CLIP's LayerNorm

@@ -451,9 +451,13 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
     const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
     const unsigned char* ssrc = grp == 0 ? a.sA : a.sW;
     const int rows = grp == 0 ? a.M : a.N;
+    // blocked A (blk_a, blk8_off; rows padded to 16): piece pc of the A stage is half pc & 1 of
+    // 16-row block pc >> 1, whose 128-deep k-tile is one contiguous 2 KB run (chunk-major image)
+    const bool ablk = grp == 0 && a.blk_a;
+    const int orows = ablk ? (a.M + 15) & ~15 : rows;
     auto rsrc_of = [&](int m0, int n0) {
         const int r0 = grp == 0 ? m0 : n0;
-        const size_t bytes = (size_t)(rows - r0) * ldb;
+        const size_t bytes = (size_t)(orows - r0) * ldb;
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
     };
     // scale dwords: one resource over the whole scale array (rows past M / N read 0), the
@@ -465,8 +469,10 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
-        voff[i] = (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
+        voff[i] = ablk ? (unsigned)((pc >> 1) * 16 * ldb + (pc & 1) * 1024 + lane * 16)
+                       : (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
     }
+    const int kshift = ablk ? 11 : 7;  // bytes per k-tile along a row (block): 2048 / 128
     const unsigned obase = (grp == 0 ? 0 : A_BYTES) + 2 * wc * 1024;  // + (8 part + i) KB
     const unsigned sbase = OPS + grp * BM * 4 + wc * 256;
 
@@ -495,7 +501,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         asm volatile("" : "+s"(ob), "+s"(sb));
         constexpr unsigned so = decltype(S)::value * STAGE;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * 128, smem + ob + so + (8 * part + i) * 1024);
+        for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk << kshift, smem + ob + so + (8 * part + i) * 1024);
         if (part == 0) raw_buffer_load_lds(ssr, (LDS_AS void*)(smem + sb + so), 4, (int)sv, kk * 4, 0, 0);
     };
 
@@ -524,11 +530,14 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
         return l;
     };
-    int aoff, woff, asoff, wsoff, c0, c1, sshift;
+    int aoff, woff, asoff, wsoff, c0, c1, ca0, ca1, sshift;
     auto lane_addrs = [&] {
         const int l = lane_id();
         const int lrow = l & 15, lsw = l & 7, lg = l >> 4;
-        aoff = (grp * 128 + lrow) * 128;
+        // A: swizzled row-major image, or (blk_a) chunk-major 16-row blocks
+        aoff = a.blk_a ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
+        ca0 = a.blk_a ? lg << 8 : ((0 | lg) ^ lsw) << 4;
+        ca1 = a.blk_a ? (4 | lg) << 8 : ((4 | lg) ^ lsw) << 4;
         woff = A_BYTES + (wc * 64 + lrow) * 128;
         asoff = OPS + (grp * 128 + lrow) * 4;
         wsoff = OPS + BM * 4 + (wc * 64 + lrow) * 4;
@@ -542,9 +551,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
     // fragment and scale reads through non-char types: with char / unsigned-int typed LDS reads
     // the compiler cannot tell them apart from the pending LDS-DMA writes and puts vmcnt(0) in
     // front of every read phase (the 16-bit kernel's bf16x8 reads do not have that problem)
-    auto frag = [&](const unsigned char* p) -> i32x8 {
-        const i32x4_t lo = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + c0));
-        const i32x4_t hi = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + c1));
+    auto frag = [&](const unsigned char* p, int o0, int o1) -> i32x8 {
+        const i32x4_t lo = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + o0));
+        const i32x4_t hi = __builtin_bit_cast(i32x4_t, *(const bf16x8*)(p + o1));
         return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     };
     auto scale = [&](const unsigned char* p) -> int {
@@ -578,12 +587,12 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         // q0: W features 0-31, A rows 0-63 of the wave's half
 #pragma unroll
         for (int f = 0; f < 2; ++f) {
-            wf[f] = frag(st + woff + f * 2048);
+            wf[f] = frag(st + woff + f * 2048, c0, c1);
             ws[f] = scale(st + wsoff + f * 64);
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            af[f] = frag(st + aoff + f * 2048);
+            af[f] = frag(st + aoff + f * 2048, ca0, ca1);
             as[f] = scale(st + asoff + f * 64);
         }
         if (grp == 0) issue(1, kt + 1, NS{}); else issue(2, kt + 1, NS{});
@@ -599,7 +608,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         // q1: W features 32-63 (last W read of this stage)
 #pragma unroll
         for (int f = 2; f < 4; ++f) {
-            wf[f] = frag(st + woff + f * 2048);
+            wf[f] = frag(st + woff + f * 2048, c0, c1);
             ws[f] = scale(st + wsoff + f * 64);
         }
         if (grp == 0) issue(2, kt + 1, NS{}); else issue(3, kt + 1, NS{});
@@ -615,7 +624,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         // q2: A rows 64-127 (last A read of this stage)
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-            af[f] = frag(st + aoff + (f + 4) * 2048);
+            af[f] = frag(st + aoff + (f + 4) * 2048, ca0, ca1);
             as[f] = scale(st + asoff + (f + 4) * 64);
         }
         if (grp == 0) issue(3, kt + 1, NS{}); else issue(0, kt + 2, PS{});
@@ -692,7 +701,8 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                 const int e = mx_exp(am);
                 const float inv = mx_inv(e);
                 if (m < a.M) {
-                    *(uint4*)((unsigned char*)a.C + (size_t)m * a.ldc + n) =
+                    // blocked C (blk_c): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes
+                    *(uint4*)((unsigned char*)a.C + (a.blk_c ? blk8_off(m, n, a.ldc) : (size_t)m * a.ldc + n)) =
                         make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
                                    pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                    pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
@@ -749,6 +759,8 @@ static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) 
 
 int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant) {
     if (a.K % 128 != 0 || a.M <= 0 || !a.sA || !a.sW) return -1;
+    if ((a.blk_a || a.blk_c) && variant != 3) return -1;  // blocked u8: the persistent ping-pong only
+    if (a.blk_c && (epi != EPI_GELU_Q8 || a.ldc % 128)) return -1;
     if ((epi == EPI_GELU_Q8 || epi == EPI_Q8) && (!a.sC || a.ldc % 32)) return -1;
     if (out16 == 2) return launch_mx8_t<F16>(s, epi, a, variant);
     return launch_mx8_t<BF16>(s, epi, a, variant);
