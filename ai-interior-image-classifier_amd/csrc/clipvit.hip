@@ -424,8 +424,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
-    a.blk_c = h->u_blk && role == R_FC;  // every R_FC output / R_PROJ input is the lane's u
-    a.blk_a = h->u_blk && role == R_PROJ;
+    // every R_FC output / R_PROJ input is the lane's u; forced single-buffer tiles (1-3) and
+    // stream-K cannot address the blocked layout, so those keep u row-major for both roles
+    auto blk_ok = [](int v) { return v >= 8 && v != 65; };
+    const bool ublk = h->u_blk && (!h->var_forced || (blk_ok(h->var[R_FC]) && blk_ok(h->var[R_PROJ])));
+    a.blk_c = ublk && role == R_FC;
+    a.blk_a = ublk && role == R_PROJ;
     int variant = h->var[role];
     // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
     // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
@@ -534,12 +538,12 @@ static int patch_embed(clipvit_handle* h, hipStream_t s, const void* pix, int in
 // MX-fp8 GEMM: A = (A8, A8 + M*K scales), W = packed (N*K e4m3 bytes, then scales).
 static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char* A8,
                  const void* Wq, const float* bias, void* C, int M, int N, int K, int ldc,
-                 int role) {
+                 int role, bool ublk = false) {
     GemmArgs a{};
-    // u8 (c_fc -> c_proj) in the 16-row blocked layout (blk8_off): its scales follow the padded
-    // rows, since the last block's real rows spread over the whole block
-    a.blk_c = h->u_blk && role == R_FC;
-    a.blk_a = h->u_blk && role == R_PROJ;
+    // ublk: u8 (c_fc -> c_proj) in the 16-row blocked layout (blk8_off); its scales follow the
+    // padded rows, since the last block's real rows spread over the whole block
+    a.blk_c = ublk && role == R_FC;
+    a.blk_a = ublk && role == R_PROJ;
     const size_t ma = a.blk_a ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
     const size_t mc = a.blk_c ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
     a.A = A8; a.sA = A8 + ma * K;
@@ -673,14 +677,17 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         if (r16) add_ln(y, nullptr, ly.ln2g, ly.ln2b, qm, defer);
         else ln(ly.ln2g, ly.ln2b, qm);
         if (prof) prof->mark(s, F_LN);
-        rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC)
+        const bool p16 = r16 && !last;
+        // blocked u8: both MLP GEMMs on the persistent MX tile, whose epilogues are STORE / GELU_Q8
+        // (the fp32 residual c_proj runs on the other MX tiles: row-major u8)
+        const bool ublk = h->u_blk && p16 && h->var8[R_FC] == 3 && h->var8[R_PROJ] == 3;
+        rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC, ublk)
                : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w);
         if (rc) return rc;
         if (prof) prof->mark(s, F_FC);
-        const bool p16 = r16 && !last;
         const int ep = p16 ? EPI_STORE : EPI_RESID;
         void* cp = p16 ? (defer ? y2 : y) : (void*)w->x;
-        rc = qm ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ)
+        rc = qm ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ, ublk)
                : gemm(s, h, ep, w->u, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ);
         if (rc) return rc;
         if (prof) prof->mark(s, F_PROJ);

@@ -370,7 +370,8 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu):
     ("ViT-B/16", "fp16", 64, {}),               # N = 197, round split
     ("ViT-L/14@336px", "fp16", 32, {}),         # large M: persistent v63 writes and reads u
     ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3463,80"}),  # v8 direct stores, v80 reads
-    ("ViT-B/32", "mxfp8", 64, {}),              # the 16-bit blocks of the MX-fp8 forward
+    ("ViT-B/32", "mxfp8", 64, {}),              # MX-fp8: fp8 u of the MX blocks, 16-bit u of the rest
+    ("ViT-B/32", "mxfp8", 64, {"mx8_skip": ""}),  # every block MX; the last c_proj keeps u row-major
 ])
 def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
     """The c_fc -> c_proj intermediate in the 16-row blocked layout (default; tuning u_blocked=0:
