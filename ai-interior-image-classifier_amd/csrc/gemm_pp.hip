@@ -38,10 +38,11 @@ namespace clipvit {
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
 
-template <typename T, int EPI, bool NT = false>
+template <typename T, int EPI, bool NT = false, bool PF = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
+    constexpr int PFD = 3;  // PF: k-tiles ahead of the one in flight
     constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
     constexpr int NBIAS = 8192;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 160 KB
@@ -70,6 +71,11 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     const bool ablk = grp == 0 && a.blk_a;
     const int rows = grp == 0 ? (a.blk_a ? (a.M + 15) & ~15 : a.M) : a.N;
     auto rsrc_of = [&](int m0, int n0) {
+#if CLIPVIT_ABLATE == 4 || CLIPVIT_ABLATE == 5 || CLIPVIT_ABLATE == 6
+        // diagnostic builds only (tools/exp_l2.sh): every tile stages the first A panel (5), the
+        // first W panel (6) or both (4), so those operands stay L2-resident (outputs are garbage)
+        if ((CLIPVIT_ABLATE != 6 && grp == 0) || (CLIPVIT_ABLATE != 5 && grp == 1)) m0 = n0 = 0;
+#endif
         const int r0 = grp == 0 ? m0 : n0;
         const size_t bytes = (size_t)(rows - r0) * ldb;
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
@@ -101,6 +107,25 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         unsigned char* dst = smem + (j & 1) * STAGE + opbase;  // nk even: the stream's parity
 #pragma unroll
         for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * kstride, dst + (8 * part + 2 * wc + i) * 1024);
+    };
+    // PF (variant 66): L2 prefetch of k-tile j. Wave wc of group g touches one dword of each of
+    // the 64 lines of its 64 rows of that k-tile's A (g = 0) or W (g = 1) slice by a 4-byte
+    // LDS-DMA into a scratch run at the end of the bias area (never read; N <= 8128), so the
+    // slice's L2 misses start about a k-tile before its staging pieces are issued. Counted by
+    // vmcnt like the pieces: issued right after the group's wait, it must land by the next one.
+    const unsigned tvoff = ablk ? (unsigned)((4 * wc + (lane >> 4)) * 16 * ldb + (lane & 15) * 128)
+                                : (unsigned)((64 * wc + lane) * ldb);
+    auto touch = [&](int j) {
+        if constexpr (PF) {
+            i32x4_t r = rs_c;
+            int kk = j;
+            if (j >= nk) {
+                if (!has_next || j >= 2 * nk) return;
+                r = rs_n;
+                kk = j - nk;
+            }
+            raw_buffer_load_lds(r, (LDS_AS void*)(smem + 2 * STAGE + NBIAS * 4 - 256), 4, (int)tvoff, kk * kstride, 0, 0);
+        }
     };
 
     f32x4 acc[4][8];
@@ -207,6 +232,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         } else {
             issue(1, kt + 2);
             if (more) vm_wait<4>(); else vm_wait<0>();
+            touch(kt + PFD);
         }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -222,6 +248,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 0) {
             if (more) vm_wait<2>(); else vm_wait<0>();
+            touch(kt + PFD);
         }
         __builtin_amdgcn_s_barrier();
     };
@@ -632,13 +659,14 @@ __global__ __launch_bounds__(512, 1) void gemm_psk_kernel(GemmArgs a, int ntiles
     if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 }
 
-template <typename T, bool NT>
+template <typename T, bool NT, bool PF = false>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (PF && a.N > 8128) return -1;  // the touch scratch sits behind the bias vector
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, PF><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, PF><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
@@ -658,13 +686,14 @@ static int launch_psk_t(hipStream_t s, int epi, const GemmArgs& a) {
 }
 
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
-// non-temporal stores; 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
+// non-temporal stores; 66: 62 with L2 prefetch touches (PF); 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
 // would be shorter than one tile's k-tiles)
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
     if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
     if (variant == 65) return dtype == 2 ? launch_psk_t<F16>(s, epi, a) : launch_psk_t<BF16>(s, epi, a);
     if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
+    if (variant == 66) return dtype == 2 ? launch_ppp_t<F16, false, true>(s, epi, a) : launch_ppp_t<BF16, false, true>(s, epi, a);
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     return -1;
 }
