@@ -38,7 +38,7 @@ namespace clipvit {
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
 
-template <typename T, int EPI, bool NT = false, bool PF = false, bool FL = false>
+template <typename T, int EPI, bool NT = false, bool PF = false, bool FL = false, bool FW = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -134,6 +134,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     // slots more lead before the wait; the wait that retires k-tile j + 1 then leaves k-tile
     // j + 2's six pieces in flight
     constexpr int A_LEFT = FL ? 6 : 2;
+    // FW (variants 69 / 70): group 1 stages all four W parts of k-tile j + 2 in its P2 / P3 read
+    // slots (two parts each; W rows are free once group 1's P1 reads retired) instead of parts
+    // 2 / 3 one k-tile later; its wait then leaves the eight pieces of k-tile j + 2 in flight
+    constexpr int W_LEFT = FW ? 8 : 4;
     f32x4 acc[4][8];
     // prologue (as gemm_pp_kernel)
 #pragma unroll
@@ -147,11 +151,15 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     } else {
         issue(0, 1);
         issue(1, 1);
+        if (FW) {
+            issue(2, 1);
+            issue(3, 1);
+        }
     }
     // the bias vector -> LDS (ordinary loads: the compiler drains vmcnt before the LDS writes,
     // which only waits for the prologue pieces a little early)
     for (int i = tid; i < a.N; i += 512) colv[i] = a.bias ? a.bias[i] : 0.f;
-    if (grp == 0) vm_wait<A_LEFT>(); else vm_wait<4>();
+    if (grp == 0) vm_wait<A_LEFT>(); else vm_wait<W_LEFT>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
@@ -179,7 +187,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             af[f][0] = *(const vec8*)(st + aoff + f * 2048 + a0);
             af[f][1] = *(const vec8*)(st + aoff + f * 2048 + a1);
         }
-        if (grp == 0) issue(FL ? 3 : 1, kt + 1); else issue(2, kt + 1);
+        if (grp == 0) issue(FL ? 3 : 1, kt + 1); else if (!FW) issue(2, kt + 1);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -200,7 +208,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
             wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
         }
-        if (grp == 0) issue(FL ? 0 : 2, kt + FL + 1); else issue(3, kt + 1);
+        if (grp == 0) issue(FL ? 0 : 2, kt + FL + 1); else if (!FW) issue(3, kt + 1);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -221,7 +229,12 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a0);
             af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a1);
         }
-        if (grp == 0) issue(FL ? 2 : 3, kt + FL + 1); else issue(0, kt + 2);
+        if (grp == 0) {
+            issue(FL ? 2 : 3, kt + FL + 1);
+        } else {
+            issue(0, kt + 2);
+            if (FW) issue(1, kt + 2);
+        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -240,8 +253,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         if (grp == 0) {
             issue(FL ? 1 : 0, kt + 2);
         } else {
-            issue(1, kt + 2);
-            if (more) vm_wait<4>(); else vm_wait<0>();
+            issue(FW ? 2 : 1, kt + 2);
+            if (FW) issue(3, kt + 2);
+            if (more) vm_wait<W_LEFT>(); else vm_wait<0>();
             touch(kt + PFD);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -669,14 +683,14 @@ __global__ __launch_bounds__(512, 1) void gemm_psk_kernel(GemmArgs a, int ntiles
     if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 }
 
-template <typename T, bool NT, bool PF = false, bool FL = false>
+template <typename T, bool NT, bool PF = false, bool FL = false, bool FW = false>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
     if (PF && a.N > 8128) return -1;  // the touch scratch sits behind the bias vector
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, PF, FL><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, PF, FL><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, PF, FL, FW><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, PF, FL, FW><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
@@ -697,7 +711,8 @@ static int launch_psk_t(hipStream_t s, int epi, const GemmArgs& a) {
 
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
 // non-temporal stores; 66: 62 with L2 prefetch touches (PF); 67: 62 with group 0's A parts staged
-// earlier (FL); 68: both; 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
+// earlier (FL); 68: both; 69: FL + all W parts of a k-tile staged in group 1's P2 / P3 (FW); 70: FW;
+// 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
 // would be shorter than one tile's k-tiles)
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
@@ -707,6 +722,8 @@ int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int var
     if (variant == 66) return dtype == 2 ? launch_ppp_t<F16, false, true>(s, epi, a) : launch_ppp_t<BF16, false, true>(s, epi, a);
     if (variant == 67) return dtype == 2 ? launch_ppp_t<F16, false, false, true>(s, epi, a) : launch_ppp_t<BF16, false, false, true>(s, epi, a);
     if (variant == 68) return dtype == 2 ? launch_ppp_t<F16, false, true, true>(s, epi, a) : launch_ppp_t<BF16, false, true, true>(s, epi, a);
+    if (variant == 69) return dtype == 2 ? launch_ppp_t<F16, false, false, true, true>(s, epi, a) : launch_ppp_t<BF16, false, false, true, true>(s, epi, a);
+    if (variant == 70) return dtype == 2 ? launch_ppp_t<F16, false, false, false, true>(s, epi, a) : launch_ppp_t<BF16, false, false, false, true>(s, epi, a);
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     return -1;
 }
