@@ -28,6 +28,15 @@
 
 namespace clipvit {
 
+#if CLIPVIT_ABLATE == 9 || CLIPVIT_ABLATE == 10
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+template <typename T>
+__device__ __forceinline__ f32x16 mfma32(const typename T::vec8& a, const typename T::vec8& b, const f32x16& c) {
+    if constexpr (std::is_same<T, F16>::value) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+#endif
+
 // ---------------------------------------------------------------------------------------
 // Persistent form (variant 62): one workgroup per CU walks the tiles blockIdx.x, blockIdx.x + G,
 // ... (G = grid size; logical ids through the same bijective XCD remap, so every XCD group
@@ -97,6 +106,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     i32x4_t rs_c = rsrc_of(m0, n0), rs_n = has_next ? rsrc_of(mn, nn) : rs_c;
     // k-tile j of the current tile's frame (j >= nk: k-tile j - nk of the next tile)
     auto issue = [&](int part, int j) {
+#if CLIPVIT_ABLATE == 7 || CLIPVIT_ABLATE == 10  // diagnostic builds only (tools/exp_l2.sh): no staging after the first two k-tiles
+        if (j >= 2) return;
+#endif
         i32x4_t r = rs_c;
         int kk = j;
         if (j >= nk) {
@@ -174,6 +186,25 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 
     // one k-tile (4 phases); Z: the tile's first k-tile (k-half 0 MFMAs start from zero)
+#if CLIPVIT_ABLATE == 8  // diagnostic build only (tools/exp_l2.sh): no MFMAs (fragments kept live)
+#define MFMA_OR_SINK(C, Wf, Af, ZERO, S, I) asm volatile("" ::"v"(Wf), "v"(Af))
+#elif CLIPVIT_ABLATE == 9 || CLIPVIT_ABLATE == 10
+    // diagnostic builds only (tools/exp_l2.sh): every pair of 16x16x32 MFMAs (same FLOPs, same
+    // matrix-pipe cycles) replaced by one 32x32x16 MFMA into scratch accumulators (half the MFMA
+    // issue slots; outputs are garbage); 10: also no staging after the first two k-tiles
+#define MFMA_OR_SINK(C, Wf, Af, ZERO, S, I)                  \
+    do {                                                     \
+        if ((S) == 0) dacc[(I) & 3] = mfma32<T>(Wf, Af, dacc[(I) & 3]); \
+        else asm volatile("" ::"v"(Wf), "v"(Af));           \
+    } while (0)
+    f32x16 dacc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) dacc[i][j] = 0.f;
+#else
+#define MFMA_OR_SINK(C, Wf, Af, ZERO, S, I) C = T::mfma16(Wf, Af, (ZERO) ? zero : C)
+#endif
     auto ktile = [&](const int kt, const unsigned char* st, auto Zc) {
         constexpr bool Z = decltype(Zc)::value;
         const bool more = kt + 2 < nk || has_next;
@@ -199,7 +230,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
-                    acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm]);
+                    MFMA_OR_SINK(acc[fn][fm], wf[fn][s], af[fm][s], Z && s == 0, s, fn * 4 + fm);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -220,7 +251,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             for (int fn = 2; fn < 4; ++fn)
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
-                    acc[fn][fm] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm]);
+                    MFMA_OR_SINK(acc[fn][fm], wf[fn][s], af[fm][s], Z && s == 0, s, fn * 4 + fm);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -246,7 +277,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             for (int fn = 2; fn < 4; ++fn)
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
-                    acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm + 4]);
+                    MFMA_OR_SINK(acc[fn][fm + 4], wf[fn][s], af[fm][s], Z && s == 0, s, fn * 4 + fm);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -267,7 +298,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             for (int fn = 0; fn < 2; ++fn)
 #pragma unroll
                 for (int fm = 0; fm < 4; ++fm)
-                    acc[fn][fm + 4] = T::mfma16(wf[fn][s], af[fm][s], Z && s == 0 ? zero : acc[fn][fm + 4]);
+                    MFMA_OR_SINK(acc[fn][fm + 4], wf[fn][s], af[fm][s], Z && s == 0, s, fn * 4 + fm);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 0) {
@@ -277,6 +308,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         __builtin_amdgcn_s_barrier();
     };
 
+#undef MFMA_OR_SINK
+#if CLIPVIT_ABLATE == 8 || CLIPVIT_ABLATE == 9 || CLIPVIT_ABLATE == 10
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) acc[f][m] = zero;
+#endif
     constexpr bool GELU = EPI == EPI_GELU;
     unsigned char* const Cb = (unsigned char*)a.C;
     for (int i = 1;; ++i) {
@@ -339,6 +377,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         has_next = tile(i + 1, mn, nn);
         if (has_next) rs_n = rsrc_of(mn, nn);
     }
+#if CLIPVIT_ABLATE == 9 || CLIPVIT_ABLATE == 10
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(dacc[i]));
+#endif
     if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 }
 

@@ -64,6 +64,9 @@ def parse():
     p.add_argument("--inflight", type=int, default=1, help="batches in flight on separate HIP streams")
     p.add_argument("--cpu-seconds", type=float, default=16.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-parity", action="store_true",
+                   help="skip the parity legs (profiling runs: config 5's bf16 reference engine would "
+                        "otherwise add its own dispatches to the trace)")
     p.add_argument("--profile-iters", type=int, default=5)
     p.add_argument("--traffic-json", default=None,
                    help="PMC traffic of this command's c_fc launches (tools/profile_round.sh)")
@@ -394,7 +397,7 @@ def main():
     }
     if rccl:
         line.update(rccl)
-    if rank == 0 and a.lora_rank is not None:
+    if rank == 0 and a.lora_rank is not None and not a.no_parity:
         err = parity_check(eng, px, T, cfg)
         if a.dtype == "mxfp8":  # config 5: "logits within 2e-2 of bf16"
             p5 = parity_config5(eng, px, T, cfg, dev)

@@ -9,7 +9,7 @@ TAG=${2:-rXX}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-A="--dtype mxfp8 --batch 512 --no-cpu-baseline"
+A="--dtype mxfp8 --batch 512 --no-cpu-baseline --no-parity"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/kt" -o run \
   -- python3 "$ROOT/bench.py" $A --steps 5 --warmup 2 --profile-iters 2 > "$ROOT/$OUT/kt.log" 2>&1
 timeout -s KILL 200 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d "$ROOT/$OUT/mfma" -o run \
