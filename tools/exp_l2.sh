@@ -28,7 +28,7 @@ if [ "$1" = build ]; then
   exit 0
 fi
 SHAPES=${SHAPES:-"10752,3072,768,1;12800,2304,768,0"}
-for lib in ${LIBS:-shipped l2a l2w l2aw nostage nomfma}; do
+for lib in ${LIBS:-shipped nostage nomfma m32 m32nostage}; do
   L=""; [ $lib != shipped ] && L=$R/abx/$lib.so
   for g in ${GRIDS:-256 64}; do
     echo "== $lib grid $g"
