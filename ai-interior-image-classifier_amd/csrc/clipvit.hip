@@ -1080,7 +1080,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || (m[0] >= 66 && m[0] <= 70));
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "split_xcd") ok = parse_int(v, h->split_xcd);
@@ -1540,7 +1540,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 / 65 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || (variant >= 65 && variant <= 70);
+                        variant == 63 || variant == 65;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

@@ -857,7 +857,7 @@ int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int varian
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
-    if (variant >= 62 && variant <= 70) return launch_gemm_pp(s, dtype, epi, a, variant);
+    if (variant >= 62 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);

@@ -47,11 +47,10 @@ __device__ __forceinline__ f32x16 mfma32(const typename T::vec8& a, const typena
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
 
-template <typename T, int EPI, bool NT = false, bool PF = false, bool FL = false, bool FW = false>
+template <typename T, int EPI, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
-    constexpr int PFD = 3;  // PF: k-tiles ahead of the one in flight
     constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
     constexpr int NBIAS = 8192;
     __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE + NBIAS * 4];  // 160 KB
@@ -120,58 +119,20 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
 #pragma unroll
         for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk * kstride, dst + (8 * part + 2 * wc + i) * 1024);
     };
-    // PF (variant 66): L2 prefetch of k-tile j. Wave wc of group g touches one dword of each of
-    // the 64 lines of its 64 rows of that k-tile's A (g = 0) or W (g = 1) slice by a 4-byte
-    // LDS-DMA into a scratch run at the end of the bias area (never read; N <= 8128), so the
-    // slice's L2 misses start about a k-tile before its staging pieces are issued. Counted by
-    // vmcnt like the pieces: issued right after the group's wait, it must land by the next one.
-    const unsigned tvoff = ablk ? (unsigned)((4 * wc + (lane >> 4)) * 16 * ldb + (lane & 15) * 128)
-                                : (unsigned)((64 * wc + lane) * ldb);
-    auto touch = [&](int j) {
-        if constexpr (PF) {
-            i32x4_t r = rs_c;
-            int kk = j;
-            if (j >= nk) {
-                if (!has_next || j >= 2 * nk) return;
-                r = rs_n;
-                kk = j - nk;
-            }
-            raw_buffer_load_lds(r, (LDS_AS void*)(smem + 2 * STAGE + NBIAS * 4 - 256), 4, (int)tvoff, kk * kstride, 0, 0);
-        }
-    };
-
-    // FL (variants 67 / 68): group 0 stages each A part of k-tile j + 2 in the first read slot
-    // after its rows were last read and retired (P1: rows 0-63, P2: 128-191, P3: 64-127, next
-    // P0: 192-255) instead of parts 1-3 one k-tile later: the same two pieces per phase, 2-6
-    // slots more lead before the wait; the wait that retires k-tile j + 1 then leaves k-tile
-    // j + 2's six pieces in flight
-    constexpr int A_LEFT = FL ? 6 : 2;
-    // FW (variants 69 / 70): group 1 stages all four W parts of k-tile j + 2 in its P2 / P3 read
-    // slots (two parts each; W rows are free once group 1's P1 reads retired) instead of parts
-    // 2 / 3 one k-tile later; its wait then leaves the eight pieces of k-tile j + 2 in flight
-    constexpr int W_LEFT = FW ? 8 : 4;
     f32x4 acc[4][8];
     // prologue (as gemm_pp_kernel)
 #pragma unroll
     for (int p = 0; p < 4; ++p) issue(p, 0);
     if (grp == 0) {
         issue(0, 1);
-        if (FL) {
-            issue(2, 1);
-            issue(1, 1);
-        }
     } else {
         issue(0, 1);
         issue(1, 1);
-        if (FW) {
-            issue(2, 1);
-            issue(3, 1);
-        }
     }
     // the bias vector -> LDS (ordinary loads: the compiler drains vmcnt before the LDS writes,
     // which only waits for the prologue pieces a little early)
     for (int i = tid; i < a.N; i += 512) colv[i] = a.bias ? a.bias[i] : 0.f;
-    if (grp == 0) vm_wait<A_LEFT>(); else vm_wait<W_LEFT>();
+    if (grp == 0) vm_wait<2>(); else vm_wait<4>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
@@ -218,7 +179,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             af[f][0] = *(const vec8*)(st + aoff + f * 2048 + a0);
             af[f][1] = *(const vec8*)(st + aoff + f * 2048 + a1);
         }
-        if (grp == 0) issue(FL ? 3 : 1, kt + 1); else if (!FW) issue(2, kt + 1);
+        if (grp == 0) issue(1, kt + 1); else issue(2, kt + 1);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -239,7 +200,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             wf[f][0] = *(const vec8*)(st + woff + f * 2048 + c0);
             wf[f][1] = *(const vec8*)(st + woff + f * 2048 + c1);
         }
-        if (grp == 0) issue(FL ? 0 : 2, kt + FL + 1); else if (!FW) issue(3, kt + 1);
+        if (grp == 0) issue(2, kt + 1); else issue(3, kt + 1);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -260,12 +221,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
             af[f][0] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a0);
             af[f][1] = *(const vec8*)(st + aoff + (f + 4) * 2048 + a1);
         }
-        if (grp == 0) {
-            issue(FL ? 2 : 3, kt + FL + 1);
-        } else {
-            issue(0, kt + 2);
-            if (FW) issue(1, kt + 2);
-        }
+        if (grp == 0) issue(3, kt + 1); else issue(0, kt + 2);
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -282,12 +238,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         if (grp == 0) {
-            issue(FL ? 1 : 0, kt + 2);
+            issue(0, kt + 2);
         } else {
-            issue(FW ? 2 : 1, kt + 2);
-            if (FW) issue(3, kt + 2);
-            if (more) vm_wait<W_LEFT>(); else vm_wait<0>();
-            touch(kt + PFD);
+            issue(1, kt + 2);
+            if (more) vm_wait<4>(); else vm_wait<0>();
         }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -302,8 +256,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 0) {
-            if (more) vm_wait<A_LEFT>(); else vm_wait<0>();
-            touch(kt + PFD);
+            if (more) vm_wait<2>(); else vm_wait<0>();
         }
         __builtin_amdgcn_s_barrier();
     };
@@ -725,14 +678,13 @@ __global__ __launch_bounds__(512, 1) void gemm_psk_kernel(GemmArgs a, int ntiles
     if (grp == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 }
 
-template <typename T, bool NT, bool PF = false, bool FL = false, bool FW = false>
+template <typename T, bool NT>
 static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (PF && a.N > 8128) return -1;  // the touch scratch sits behind the bias vector
-    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, PF, FL, FW><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, PF, FL, FW><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;
 }
 
@@ -752,20 +704,13 @@ static int launch_psk_t(hipStream_t s, int epi, const GemmArgs& a) {
 }
 
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
-// non-temporal stores; 66: 62 with L2 prefetch touches (PF); 67: 62 with group 0's A parts staged
-// earlier (FL); 68: both; 69: FL + all W parts of a k-tile staged in group 1's P2 / P3 (FW); 70: FW;
-// 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
+// non-temporal stores; 65: stream-K (a.sk_part / a.sk_flag workspace; whole tiles where a share
 // would be shorter than one tile's k-tiles)
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
     if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
     if (variant == 65) return dtype == 2 ? launch_psk_t<F16>(s, epi, a) : launch_psk_t<BF16>(s, epi, a);
     if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
-    if (variant == 66) return dtype == 2 ? launch_ppp_t<F16, false, true>(s, epi, a) : launch_ppp_t<BF16, false, true>(s, epi, a);
-    if (variant == 67) return dtype == 2 ? launch_ppp_t<F16, false, false, true>(s, epi, a) : launch_ppp_t<BF16, false, false, true>(s, epi, a);
-    if (variant == 68) return dtype == 2 ? launch_ppp_t<F16, false, true, true>(s, epi, a) : launch_ppp_t<BF16, false, true, true>(s, epi, a);
-    if (variant == 69) return dtype == 2 ? launch_ppp_t<F16, false, false, true, true>(s, epi, a) : launch_ppp_t<BF16, false, false, true, true>(s, epi, a);
-    if (variant == 70) return dtype == 2 ? launch_ppp_t<F16, false, false, false, true>(s, epi, a) : launch_ppp_t<BF16, false, false, false, true>(s, epi, a);
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     return -1;
 }

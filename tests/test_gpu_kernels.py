@@ -34,11 +34,10 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # of the k-tile iterations, split tiles combined through fp32 partial slots; whole tiles where a
 # share would be shorter than one tile's k-tiles);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 22, 62, 63, 65, 66, 67, 68, 69, 70, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463,
-            3465, 3466, 3467, 3468, 3469, 3470, 3480]
+VARIANTS = [1, 2, 3, 8, 22, 62, 63, 65, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3465, 3480]
 N128 = (1, 2, 22, 81, 82)
-N256 = (3, 8, 62, 63, 65, 66, 67, 68, 69, 70, 80, 98)
-STAGED = (62, 63, 65, 66, 67, 68, 69, 70, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 62, 63, 65, 80, 98)
+STAGED = (62, 63, 65, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -53,7 +52,7 @@ def _skip(variant, N, K):
     v = variant % 100
     if (v in N128 and N % 128) or (v in N256 and N % 256):
         return "tile does not divide N"
-    if v in (62, 63, 65, 66, 67, 68, 69, 70) and K % 128:
+    if v in (62, 63, 65) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
     return None
 
@@ -246,7 +245,7 @@ def test_attention_tail_rows_never_read(gpu, B, N, H, causal):
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
                                    (36928 // 4, 4096, 1024)])
 def test_ping_pong_race_screen(gpu, M, N, K):
-    """The persistent ping-pong GEMMs (62, 63, 66-70) hand LDS stages between waves by counted vmcnt and
+    """The persistent ping-pong GEMMs (62, 63) hand LDS stages between waves by counted vmcnt and
     barriers only. Every accumulator sees the same k order as the 2-phase 256x256 tile (v8), so
     the outputs must equal v8's bit for bit on every one of many repeated launches: a read that
     overtook its DMA (or a refill that overtook a read) would show as a differing tile."""
@@ -256,7 +255,7 @@ def test_ping_pong_race_screen(gpu, M, N, K):
     bias = torch.randn(N, device=gpu, generator=g)
     for epi in (10, 11):  # 16-bit store / QuickGELU
         ref = E.gemm_test(A, W, bias, epi=epi, variant=8)
-        for variant in (62, 63, 66, 67, 68, 69, 70, 3462, 3463, 3466, 3467, 3468, 3469, 3470):
+        for variant in (62, 63, 3462, 3463):
             for _ in range(6):
                 C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
