@@ -32,7 +32,7 @@ for lib in ${LIBS:-shipped nostage nomfma m32 m32nostage}; do
   L=""; [ $lib != shipped ] && L=$R/abx/$lib.so
   for g in ${GRIDS:-256 64}; do
     echo "== $lib grid $g"
-    V=${VARS:-62}; [ $lib = shipped ] && V=${VARS:-62,66,67,68,69,70}
+    V=${VARS:-62}
     CLIPVIT_LIB=$L CLIPVIT_BENCH_GRID=$g timeout -k 10 100 python tools/gemm_ab.py "$SHAPES" "$V" 3 10 || exit 1
   done
 done
