@@ -187,6 +187,9 @@ struct clipvit_handle {
     // persistent ping-pong: 51.3 -> 55.8 us standalone, yet config 5 +1.5 % on two boxes (under
     // the two-lane split a kernel is priced by the CU time it holds)
     int var8[4] = {3, 5, 3, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
+    // MX c_fc whole-round row split (gemm8): tile of the tail launch (2 = 128x128, 5 = 160x128;
+    // 0 = off: one launch); tuning mx8_split_tail
+    int mx8_split_tail = 2;
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
     // four in bf16 — DESIGN.md §MX-fp8); tuning mx8_skip="..." overrides
@@ -554,6 +557,31 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.ncu = h->ncu;
     const int v8 = h->var8[role];
     if (v8 == 3 && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
+    // Whole-round row split of the MX c_fc (as gemm()'s for the 16-bit one): when the 256x256
+    // tiles fill R whole rounds plus at most half a round (B/32 lane of 256 images: 600 tiles =
+    // 2 rounds + 88), rows [0, M1) run on the persistent ping-pong and rows [M1, M) on the
+    // 128x128 tile (two per CU) as a second launch. Row-wise independent: bit-identical to one
+    // launch (same k order); the tail writes the same blocked u8 and its scales
+    if (role == R_FC && epi == EPI_GELU_Q8 && v8 == 3 && h->round_split && h->mx8_split_tail && N % 256 == 0) {
+        const long nN = N / 256, tm = (long)((M + 255) / 256) * nN;
+        const long R = tm / h->ncu, rem = tm % h->ncu;
+        const long m1 = R * h->ncu / nN * 256;
+        if (R >= 1 && rem > 0 && 2 * rem <= h->ncu && m1 > 0 && m1 < M) {
+            GemmArgs b = a, c = a;
+            b.M = (int)m1;
+            c.M = M - (int)m1;
+            c.A = A8 + (size_t)m1 * K;
+            c.sA = a.sA + (size_t)m1 * (K / 32);
+            c.C = (unsigned char*)C + (size_t)m1 * ldc;  // = blk8_off(m1, 0, ldc): m1 % 16 == 0
+            c.sC = a.sC + (size_t)m1 * (ldc / 32);
+            c.xcd_n = 0;
+            if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, b, 3) == 0 &&
+                launch_gemm_mx8(s, CLIPVIT_BF16, epi, c, h->mx8_split_tail) == 0)
+                return 0;
+            g_err = "gemm8: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
+            return CLIPVIT_E_INVALID;
+        }
+    }
     if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, v8) != 0 &&
         launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, 0) != 0) {
         g_err = "gemm8: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -1096,6 +1124,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         if (ok) h->mx8_skip_mlp = h->mx8_skip;
     } else if (k == "mx8_skip_mlp") ok = parse_mask(v, h->mx8_skip_mlp);
     else if (k == "mx8_variants") ok = parse_list(v, h->var8, 4);
+    else if (k == "mx8_split_tail") ok = parse_int(v, h->mx8_split_tail) && (h->mx8_split_tail == 0 || h->mx8_split_tail == 2 || h->mx8_split_tail == 5);
     else if (k == "large_variants") ok = parse_list(v, h->large_var, 4);
     else if (k == "stream_k") {  // role bit mask (1 QKV, 4 c_fc); 0 = off
         ok = parse_int(v, x) && x >= 0;
@@ -1129,7 +1158,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
-        int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min;
+        int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
         unsigned sk_roles;
@@ -1137,7 +1166,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
               g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
-              g->split_min, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
+              g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
         memcpy(t.large_var, g->large_var, sizeof t.large_var);
@@ -1153,6 +1182,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
+            h->mx8_split_tail = before.mx8_split_tail;
             memcpy(h->xcd, before.xcd, sizeof before.xcd);
             memcpy(h->var8, before.var8, sizeof before.var8);
             memcpy(h->large_var, before.large_var, sizeof before.large_var);

@@ -363,7 +363,8 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
                 if (m >= a.M) continue;
                 const int e = mx_exp(am);
                 const float inv = mx_inv(e);
-                *(uint4*)((unsigned char*)a.C + (size_t)m * a.ldc + n) =
+                // blocked C (blk_c, blk8_off): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes
+                *(uint4*)((unsigned char*)a.C + (a.blk_c ? blk8_off(m, n, a.ldc) : (size_t)m * a.ldc + n)) =
                     make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
                                pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
@@ -759,7 +760,10 @@ static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) 
 
 int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int variant) {
     if (a.K % 128 != 0 || a.M <= 0 || !a.sA || !a.sW) return -1;
-    if ((a.blk_a || a.blk_c) && variant != 3) return -1;  // blocked u8: the persistent ping-pong only
+    // blocked u8: read by the persistent ping-pong only; written by it or (c_fc tail launch of
+    // the whole-round row split) by the 128 x 128 / 160 x 128 tiles' QuickGELU + quantize epilogue
+    if (a.blk_a && variant != 3) return -1;
+    if (a.blk_c && variant != 3 && variant != 2 && variant != 5) return -1;
     if (a.blk_c && (epi != EPI_GELU_Q8 || a.ldc % 128)) return -1;
     if ((epi == EPI_GELU_Q8 || epi == EPI_Q8) && (!a.sC || a.ldc % 32)) return -1;
     if (out16 == 2) return launch_mx8_t<F16>(s, epi, a, variant);

@@ -109,11 +109,12 @@ def test_gemm_mx8_vs_dequantized_reference(gpu, variant, M, N, K):
     assert err < 1e-4, err
 
 
-@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("variant", [2, 3, 5])
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (12800, 768, 768), (1000, 2304, 768), (333, 3072, 768),
                                    (700, 768, 3072), (257, 512, 256)])
 def test_gemm_mx8_ping_pong_bit_identical(gpu, variant, M, N, K):
-    """The persistent 256x256 ping-pong MX tile (3) and the 160x128
+    """The persistent 256x256 ping-pong MX tile (3), the 128x128 tile (2, the MX c_fc round
+    split's tail launch) and the 160x128
     tile (5, two scale dwords per thread) accumulate every output in the same k order as the
     128x256 tile: their bf16 store and MX-fp8 (QuickGELU) output must be bit-identical to
     variant 1's, over repeated launches (race screen, as test_gpu_kernels.py's ping-pong
@@ -372,4 +373,27 @@ def test_config5_bs512_as_benched(gpu):
     finally:
         e16.close()
         e8.close()
+        one.close()
+
+
+def test_mx8_fc_round_split_is_bit_identical(gpu):
+    """The MX-fp8 c_fc whole-round row split (clipvit.hip gemm8: 256 images = 12,800 rows = 600
+    tiles of 256x256 = 2 rounds + 88; rows [0, 10752) on the persistent ping-pong, the rest on the
+    128x128 tile, both writing the blocked u8 and its scales) against one launch on the ping-pong
+    (tuning mx8_split_tail=0): logits and embeddings bit for bit."""
+    cfg = C.get_config("ViT-B/32")
+    sd = synthetic_state_dict(cfg, 0)
+    adapters = synthetic_adapters(cfg, rank=8)
+    segs = [0, 40, 60, 359, 395, 425, 437]
+    g = torch.Generator().manual_seed(77)
+    T = torch.nn.functional.normalize(torch.randn(437, cfg.embed_dim, generator=g), dim=-1)
+    px = torch.randn(256, 3, 224, 224, generator=g).clamp_(-1.8, 2.2).to(gpu)
+    split = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, 256)
+    one = _engine(cfg, "mxfp8", sd, adapters, T, segs, gpu, 256, tuning={"mx8_split_tail": 0})
+    try:
+        a, b = split.classify(px), one.classify(px)
+        torch.cuda.synchronize()
+        assert torch.equal(a.emb, b.emb) and torch.equal(a.logits, b.logits)
+    finally:
+        split.close()
         one.close()
