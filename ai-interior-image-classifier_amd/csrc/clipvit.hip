@@ -549,6 +549,8 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.blk_a = ublk && role == R_PROJ;
     const size_t ma = a.blk_a ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
     const size_t mc = a.blk_c ? (size_t)(M + 15) / 16 * 16 : (size_t)M;
+    // blocked u8 scales ([K / 128][Mpad] dwords, GemmArgs.sc_rows) go with the blocked u8
+    if (ublk && (role == R_FC || role == R_PROJ)) a.sc_rows = (int)((M + 15) / 16 * 16);
     a.A = A8; a.sA = A8 + ma * K;
     a.W = Wq; a.sW = (const unsigned char*)Wq + (size_t)N * K;
     a.bias = bias; a.C = C; a.M = M; a.N = N; a.K = K; a.ldc = ldc;
@@ -573,7 +575,7 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
             c.A = A8 + (size_t)m1 * K;
             c.sA = a.sA + (size_t)m1 * (K / 32);
             c.C = (unsigned char*)C + (size_t)m1 * ldc;  // = blk8_off(m1, 0, ldc): m1 % 16 == 0
-            c.sC = a.sC + (size_t)m1 * (ldc / 32);
+            c.sC = a.sC + (a.sc_rows ? (size_t)m1 * 4 : (size_t)m1 * (ldc / 32));
             c.xcd_n = 0;
             if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, b, 3) == 0 &&
                 launch_gemm_mx8(s, CLIPVIT_BF16, epi, c, h->mx8_split_tail) == 0)

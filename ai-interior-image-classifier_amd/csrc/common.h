@@ -183,6 +183,11 @@ struct GemmArgs {
     // Pipelined (gemm_pipe_kernel) and persistent ping-pong (62 / 63) kernels only; the others
     // refuse it. Rows are padded to a multiple of 16 in the buffer.
     int blk_a, blk_c;
+    // MX-fp8 u8 scales in the blocked form (with blk_a / blk_c): [K / 128][sc_rows] dwords, the
+    // dword of (row, 128-deep k-tile) holding its four E8M0 bytes, so a k-tile's scales of
+    // consecutive rows are one contiguous run (0 = row-major [rows][K / 32] bytes). sc_rows = the
+    // padded row count of the whole matrix (a row-split launch passes its parent's)
+    int sc_rows;
 };
 
 // 16-row blocked layout of a 16-bit [rows, ncols] matrix (ncols % 64 == 0): 16 x 64 blocks of

@@ -369,7 +369,9 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
                                pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
                                pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
-                if ((g & 1) == 0) a.sC[(size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
+                if ((g & 1) == 0)
+                    a.sC[a.sc_rows ? ((size_t)(n >> 7) * a.sc_rows + m) * 4 + ((n >> 5) & 3)
+                                   : (size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
                 continue;
             }
             if (m >= a.M) continue;
@@ -462,9 +464,16 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
     };
     // scale dwords: one resource over the whole scale array (rows past M / N read 0), the
-    // tile's row offset in the per-lane offset (VGPRs: the SGPR budget is spent)
-    const i32x4_t ssr = buf_rsrc(ssrc, (unsigned)((size_t)rows * lds_));
-    auto svoff_of = [&](int m0, int n0) { return (unsigned)(((grp == 0 ? m0 : n0) + wc * 64 + lane) * lds_); };
+    // tile's row offset in the per-lane offset (VGPRs: the SGPR budget is spent). Blocked A
+    // scales (sc_rows): [K / 128][sc_rows] dwords, so the k-tile offset is kk * sc_rows * 4 and
+    // a wave's 64 rows are one 256-B run (row-major: 64 dwords K / 32 bytes apart)
+    const bool sblk = grp == 0 && a.blk_a && a.sc_rows;
+    const i32x4_t ssr = buf_rsrc(ssrc, (unsigned)(sblk ? (size_t)a.sc_rows * (a.K / 128) * 4 : (size_t)rows * lds_));
+    const int sk_stride = sblk ? a.sc_rows * 4 : 4;  // bytes per k-tile
+    auto svoff_of = [&](int m0, int n0) {
+        const int r = (grp == 0 ? m0 : n0) + wc * 64 + lane;
+        return (unsigned)(sblk ? (size_t)r * 4 : (size_t)r * lds_);
+    };
     const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
     unsigned voff[8];
 #pragma unroll
@@ -503,7 +512,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         constexpr unsigned so = decltype(S)::value * STAGE;
 #pragma unroll
         for (int i = 0; i < 2; ++i) blds16(r, voff[2 * part + i], kk << kshift, smem + ob + so + (8 * part + i) * 1024);
-        if (part == 0) raw_buffer_load_lds(ssr, (LDS_AS void*)(smem + sb + so), 4, (int)sv, kk * 4, 0, 0);
+        if (part == 0) raw_buffer_load_lds(ssr, (LDS_AS void*)(smem + sb + so), 4, (int)sv, kk * sk_stride, 0, 0);
     };
 
     f32x4 acc[4][8];
@@ -708,7 +717,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                                    pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                    pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
                                    pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
-                    if ((eg & 1) == 0) a.sC[(size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
+                    if ((eg & 1) == 0)
+                        a.sC[a.sc_rows ? ((size_t)(n >> 7) * a.sc_rows + m) * 4 + ((n >> 5) & 3)
+                                       : (size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
                 }
             } else if (m < a.M) {  // EPI_STORE
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
