@@ -188,8 +188,11 @@ struct clipvit_handle {
     // the two-lane split a kernel is priced by the CU time it holds)
     int var8[4] = {3, 5, 3, 3};  // QKV, out_proj, c_fc, c_proj: 3 = ping-pong 256x256 (mx8.hip)
     // MX c_fc whole-round row split (gemm8): tile of the tail launch (2 = 128x128, 5 = 160x128;
-    // 0 = off: one launch); tuning mx8_split_tail
-    int mx8_split_tail = 2;
+    // 0 = off: one launch); tuning mx8_split_tail. Off: the c_fc family is 6-8 % faster per
+    // lane-forward with it (0.79 vs 0.85 ms), but config 5 runs two lanes and the tail's two
+    // workgroups per CU hold CUs the other lane would use: 117.4k / 117.7k img/s with the split
+    // against 117.9k / 118.6k without (same box, profiles/r04_ab3.txt)
+    int mx8_split_tail = 0;
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
     // four in bf16 — DESIGN.md §MX-fp8); tuning mx8_skip="..." overrides
