@@ -47,7 +47,7 @@ __device__ __forceinline__ f32x16 mfma32(const typename T::vec8& a, const typena
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
 
-template <typename T, int EPI, bool NT = false>
+template <typename T, int EPI, bool NT = false, bool BLKA = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -76,8 +76,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     const unsigned char* src = (const unsigned char*)(grp == 0 ? a.A : a.W);
     // blocked A (blk_a, blk16_off; rows padded to 16): piece pc of the A stage is half pc & 1 of
     // 16-row block pc >> 1, whose k-tile run is contiguous — the LDS image is chunk-major
-    const bool ablk = grp == 0 && a.blk_a;
-    const int rows = grp == 0 ? (a.blk_a ? (a.M + 15) & ~15 : a.M) : a.N;
+    // (BLKA compile-time: a runtime flag keeps both per-lane offset sets alive)
+    const bool ablk = BLKA && grp == 0;
+    const int rows = grp == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;
     auto rsrc_of = [&](int m0, int n0) {
 #if CLIPVIT_ABLATE == 4 || CLIPVIT_ABLATE == 5 || CLIPVIT_ABLATE == 6
         // diagnostic builds only (tools/exp_l2.sh): every tile stages the first A panel (5), the
@@ -141,8 +142,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     const int woff = A_BYTES + (wc * 64 + lrow) * 128;
     const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;
     // A fragments: swizzled row-major image, or (blk_a) chunk-major 16-row blocks
-    const int aoff = a.blk_a ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
-    const int a0 = a.blk_a ? lg << 8 : c0, a1 = a.blk_a ? (4 | lg) << 8 : c1;
+    const int aoff = BLKA ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
+    const int a0 = BLKA ? lg << 8 : c0, a1 = BLKA ? (4 | lg) << 8 : c1;
     vec8 af[4][2], wf[4][2];
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 
@@ -683,6 +684,10 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
+    if (a.blk_a) {  // blocked A (u): c_proj on the persistent tile (tuning / large-M shapes)
+        if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+        return -1;
+    }
     if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     return -1;

@@ -426,7 +426,7 @@ static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
 // part 0 is 3 VMEM ops and the counted waits are 3 (group 0) / 5 (group 1). Scale rows are
 // read with their fragments (A: q0, q2; W: q0, q1) and refilled with part 0 (group 1 at q2,
 // group 0 at q3), after the last read of each.
-template <typename TO, int EPI>
+template <typename TO, int EPI, bool BLKA = false, bool BLKC = false>
 __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int ntiles) {
     constexpr int BM = 256, BN = 256;
     constexpr int A_BYTES = BM * 128, OPS = (BM + BN) * 128, STAGE = OPS + (BM + BN) * 4;  // 66 KB
@@ -456,7 +456,10 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
     const int rows = grp == 0 ? a.M : a.N;
     // blocked A (blk_a, blk8_off; rows padded to 16): piece pc of the A stage is half pc & 1 of
     // 16-row block pc >> 1, whose 128-deep k-tile is one contiguous 2 KB run (chunk-major image)
-    const bool ablk = grp == 0 && a.blk_a;
+    // (BLKA: a compile-time choice. As a runtime flag the compiler kept both voff sets alive and
+    // spilled them in the QuickGELU + quantize instantiation; the reloads, VMEM ops under the
+    // in-order vmcnt, then waited for every staging load in flight)
+    const bool ablk = BLKA && grp == 0;
     const int orows = ablk ? (a.M + 15) & ~15 : rows;
     auto rsrc_of = [&](int m0, int n0) {
         const int r0 = grp == 0 ? m0 : n0;
@@ -467,7 +470,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
     // tile's row offset in the per-lane offset (VGPRs: the SGPR budget is spent). Blocked A
     // scales (sc_rows): [K / 128][sc_rows] dwords, so the k-tile offset is kk * sc_rows * 4 and
     // a wave's 64 rows are one 256-B run (row-major: 64 dwords K / 32 bytes apart)
-    const bool sblk = grp == 0 && a.blk_a && a.sc_rows;
+    const bool sblk = BLKA && grp == 0 && a.sc_rows;
     const i32x4_t ssr = buf_rsrc(ssrc, (unsigned)(sblk ? (size_t)a.sc_rows * (a.K / 128) * 4 : (size_t)rows * lds_));
     const int sk_stride = sblk ? a.sc_rows * 4 : 4;  // bytes per k-tile
     auto svoff_of = [&](int m0, int n0) {
@@ -475,12 +478,15 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         return (unsigned)(sblk ? (size_t)r * 4 : (size_t)r * lds_);
     };
     const int lr = lane >> 3, chunk = (lane & 7) ^ lr;
+    // 32-bit offset arithmetic (a tile's operand rows span < 4 GB): 64-bit products here were kept
+    // as register pairs and spilled in the QuickGELU + quantize instantiation
+    const unsigned ldb32 = (unsigned)ldb;
     unsigned voff[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
-        voff[i] = ablk ? (unsigned)((pc >> 1) * 16 * ldb + (pc & 1) * 1024 + lane * 16)
-                       : (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
+        const unsigned pc = 8 * (i >> 1) + 2 * wc + (i & 1);
+        voff[i] = ablk ? (pc >> 1) * 16u * ldb32 + (pc & 1) * 1024u + (unsigned)lane * 16u
+                       : (pc * 8u + (unsigned)lr) * ldb32 + (unsigned)chunk * 16u;
     }
     const int kshift = ablk ? 11 : 7;  // bytes per k-tile along a row (block): 2048 / 128
     const unsigned obase = (grp == 0 ? 0 : A_BYTES) + 2 * wc * 1024;  // + (8 part + i) KB
@@ -545,9 +551,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         const int l = lane_id();
         const int lrow = l & 15, lsw = l & 7, lg = l >> 4;
         // A: swizzled row-major image, or (blk_a) chunk-major 16-row blocks
-        aoff = a.blk_a ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
-        ca0 = a.blk_a ? lg << 8 : ((0 | lg) ^ lsw) << 4;
-        ca1 = a.blk_a ? (4 | lg) << 8 : ((4 | lg) ^ lsw) << 4;
+        aoff = BLKA ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
+        ca0 = BLKA ? lg << 8 : ((0 | lg) ^ lsw) << 4;
+        ca1 = BLKA ? (4 | lg) << 8 : ((4 | lg) ^ lsw) << 4;
         woff = A_BYTES + (wc * 64 + lrow) * 128;
         asoff = OPS + (grp * 128 + lrow) * 4;
         wsoff = OPS + BM * 4 + (wc * 64 + lrow) * 4;
@@ -681,6 +687,15 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
         const int ln = lane_id();
         const int er = ln & 15, eg = ln >> 4;
         const int n = n0 + wc * 64 + 16 * eg;
+        // blocked u8 (BLKC): offsets of the lane's row at fm = 0; fm steps 16 rows = one block
+        // row (cbs bytes) and 16 scale dwords
+        unsigned cb0 = 0, cbs = 0, sb0 = 0;
+        if constexpr (BLKC) {
+            const int mr = m0 + grp * 128 + er;
+            cb0 = (unsigned)blk8_off(mr, n, a.ldc);
+            cbs = (unsigned)(a.ldc >> 7) << 11;
+            sb0 = ((unsigned)(n >> 7) * (unsigned)a.sc_rows + (unsigned)mr) * 4u + (unsigned)((n >> 5) & 3);
+        }
         f32x4 bv[4];
         {
             const unsigned ba = (unsigned)(size_t)(LDS_AS const float*)(colv + n);
@@ -711,15 +726,23 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                 const int e = mx_exp(am);
                 const float inv = mx_inv(e);
                 if (m < a.M) {
-                    // blocked C (blk_c): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes
-                    *(uint4*)((unsigned char*)a.C + (a.blk_c ? blk8_off(m, n, a.ldc) : (size_t)m * a.ldc + n)) =
+                    // blocked C (BLKC = blk_c, compile-time: the runtime choice spilled the
+                    // accumulators): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes;
+                    // its scales [K / 128][sc_rows] dwords. 32-bit offsets (< 4 GB), fm-strided
+                    unsigned co, so;
+                    if constexpr (BLKC) {
+                        co = cb0 + (unsigned)fm * cbs;
+                        so = sb0 + (unsigned)fm * 64u;
+                    } else {
+                        co = (unsigned)m * (unsigned)a.ldc + (unsigned)n;
+                        so = (unsigned)m * (unsigned)(a.ldc / 32) + (unsigned)(n >> 5);
+                    }
+                    *(uint4*)((unsigned char*)a.C + co) =
                         make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
                                    pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                    pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
                                    pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
-                    if ((eg & 1) == 0)
-                        a.sC[a.sc_rows ? ((size_t)(n >> 7) * a.sc_rows + m) * 4 + ((n >> 5) & 3)
-                                       : (size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
+                    if ((eg & 1) == 0) a.sC[so] = (unsigned char)(e + 127);
                 }
             } else if (m < a.M) {  // EPI_STORE
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
@@ -749,8 +772,14 @@ static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persist
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = persistent && ntiles > ncu ? ncu : ntiles;
+    if (epi == EPI_STORE && a.blk_a) { gemm_mx8_pp_kernel<TO, EPI_STORE, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
     if (epi == EPI_STORE) { gemm_mx8_pp_kernel<TO, EPI_STORE><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
-    if (epi == EPI_GELU_Q8) { gemm_mx8_pp_kernel<TO, EPI_GELU_Q8><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU_Q8 && !a.blk_a) {
+        if (a.blk_c != (a.sc_rows != 0)) return -1;  // blocked u8 goes with its blocked scales
+        if (a.blk_c) gemm_mx8_pp_kernel<TO, EPI_GELU_Q8, false, true><<<grid, 512, 0, s>>>(a, ntiles);
+        else gemm_mx8_pp_kernel<TO, EPI_GELU_Q8><<<grid, 512, 0, s>>>(a, ntiles);
+        return 0;
+    }
     return -1;
 }
 
