@@ -257,7 +257,6 @@ struct clipvit_handle {
     // accumulator-layout stores become 256-B runs per quarter-wave instead of 16 scattered
     // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
     bool u_blk = true;
-    bool qkv_pp = false;  // A/B: QKV on the persistent ping-pong tile (tuning qkv_pp)
 };
 
 static std::string L(int i, const char* leaf) {
@@ -494,13 +493,6 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
         }
-    }
-    // QKV on the persistent ping-pong tile with the column-group-major map (tuning qkv_pp=1, A/B)
-    if (h->qkv_pp && !h->var_forced && role == R_QKV && epi == EPI_STORE && t256 && t256 < 4L * h->ncu) {
-        GemmArgs b = a;
-        b.xcd_n = h->split_xcd;
-        if (xcd_split_n(N / 256, b.xcd_n)) b.xcd_n = 0;
-        if (launch_gemm(s, h->dt, epi, b, 62) == 0) return 0;
     }
     // (c_fc's QuickGELU epilogue stores directly from the accumulators, v8: measured L/14@336
     // c_fc 7.79 -> 7.52 ms, B/16 1.59 -> 1.52 ms per lane-forward against the LDS-staged v80)
@@ -1119,7 +1111,6 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
-    else if (k == "qkv_pp") ok = flag(h->qkv_pp);
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63)
         int m[2] = {h->split_main, h->split_tail};
         ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
@@ -1171,7 +1162,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, qkv_pp;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
         int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
@@ -1179,7 +1170,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->qkv_pp, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
+              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
@@ -1194,7 +1185,6 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->qkv_pp = before.qkv_pp;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
             h->mx8_split_tail = before.mx8_split_tail;
