@@ -185,8 +185,10 @@ def main():
              "each, same command): MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8",
              "XCDs); MFMA busy x 2.5166 PF/s = the MFMA-issue rate the counters saw; wait = SQ_WAIT_ANY /",
              "SQ_WAVE_CYCLES (wave-cycles parked on a counter or barrier); L2 hit = TCC_HIT / (HIT + MISS).", "",
-             "| role | isolated dispatches | avg us | TFLOP/s | frac of 2.5166 PF | concurrent avg us | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | algorithmic MB | PMC / algorithmic | MFMA busy | wait | L2 hit |",
-             "|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
+             "PMC GB/s = (FETCH_SIZE x2 + WRITE_SIZE) / avg: the bytes the L2 exchanged with the fabric",
+             "(HBM or Infinity Cache) per second, against the 8 TB/s HBM3E peak (≈6.3 TB/s achievable).", "",
+             "| role | isolated dispatches | avg us | TFLOP/s | frac of 2.5166 PF | concurrent avg us | FETCH_SIZE x2 (MB) | WRITE_SIZE (MB) | PMC GB/s | frac of 8 TB/s | algorithmic MB | PMC / algorithmic | MFMA busy | wait | L2 hit |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     traffic = {}
     for role in sorted(set(dur) | set(dur_c), key=lambda k: -sum(dur.get(k, [])) - sum(dur_c.get(k, []))):
         d = dur.get(role) or dur_c[role]
@@ -205,7 +207,8 @@ def main():
                          "wait_share": wt, "l2_hit": l2}
         al = f"{algo[role] / 1e6:.1f}" if role in algo else ""
         ratio = f"{(fb + wb) * 1e6 / algo[role]:.2f}" if role in algo else ""
-        lines.append(f"| {role} | {len(dur.get(role, []))} | {avg:.1f} | {tf} | {fr} | {cavg} | {fb:.1f} | {wb:.1f} | {al} | {ratio} "
+        gbs = (fb + wb) * 1e6 / (avg * 1e-6) / 1e9
+        lines.append(f"| {role} | {len(dur.get(role, []))} | {avg:.1f} | {tf} | {fr} | {cavg} | {fb:.1f} | {wb:.1f} | {gbs:.0f} | {gbs / 8000:.2f} | {al} | {ratio} "
                      f"| {mb:.3f} | {wt:.3f} | {l2:.3f} |")
     if "fc_tail" in traffic:  # one c_fc invocation = main + tail launch
         a, b = traffic["fc"], traffic.pop("fc_tail")
@@ -215,9 +218,10 @@ def main():
             traffic["fc"][k] = (a[k] * wa + b[k] * wb_) / (wa + wb_)
         t = traffic["fc"]
         fl, al = flops["fc"] + flops["fc_tail"], algo["fc"] + algo["fc_tail"]
+        gbs = (t['read_bytes'] + t['write_bytes']) / (t['avg_us'] * 1e-6) / 1e9
         lines.append(f"| fc (main + tail) | | {t['avg_us']:.1f} | {fl / (t['avg_us'] * 1e-6) / 1e12:.0f} | "
                      f"{fl / (t['avg_us'] * 1e-6) / 2.5166e15:.3f} | | "
-                     f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} | {al / 1e6:.1f} | "
+                     f"{t['read_bytes'] / 1e6:.1f} | {t['write_bytes'] / 1e6:.1f} | {gbs:.0f} | {gbs / 8000:.2f} | {al / 1e6:.1f} | "
                      f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} | {t['mfma_busy']:.3f} | {t['wait_share']:.3f} | "
                      f"{t['l2_hit']:.3f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
