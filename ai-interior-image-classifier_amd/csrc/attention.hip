@@ -7,181 +7,37 @@
 // Layout: qkv [B*N, 3*D] (16-bit, output of the QKV GEMM; q | k | v, head h at cols h*64),
 //         out [B*N, D]   (16-bit, head h at cols h*64) -> input of the out_proj GEMM.
 //
-// One workgroup = 4 waves = 64 query rows of one (image, head); each wave owns 16 queries.
+// One workgroup = 4 waves = 64 query rows of one (image, head) (attention_v2_kernel; each wave
+// owns 16 queries) or 128 query rows (attention_v3_kernel, N > 128: 32 queries per wave).
 // Keys/values are streamed in blocks of 64 through LDS with an online (flash-style) softmax,
-// so any token count works: N = 50 (B/32), 197 (B/16), 577 (L/14@336).
+// so any token count works: N = 50 (B/32, one key block), 77 (text, causal), 197 (B/16),
+// 577 (L/14@336).
 //   S^T[key][q] = mfma(K rows, Q rows)  -> lane (q = lane&15, g = lane>>4) holds 16 keys of
 //                                           its own query: the row max/sum are 15 local ops +
 //                                           two xor-shuffles (lanes q, q+16, q+32, q+48);
 //   O^T[d][q]  += mfma(V^T, P^T)         -> P^T is consumed straight from the S registers
 //                                           (permuted k order, matched on the V side), no LDS
 //                                           round trip for P.
-// K in LDS: 128-B rows, 16-B chunk swizzle c ^ (row & 7) (conflict-free ds_read_b128).
-// V in LDS transposed (Vt[d][key]), 8-B chunk swizzle (key/4) ^ 2*((d>>1)&7): each
-// ds_read_b64 of a V^T fragment is conflict-free.
-#include <cstdlib>
-
+// K and V in LDS: 128-B rows, 16-B chunk swizzle c ^ (row & 7) (conflict-free ds_read_b128);
+// V is read transposed by ds_read_b64_tr_b16.
 #include "common.h"
 
 namespace clipvit {
 
-// CAUSAL (text tower, CLIP.build_attention_mask: -inf above the diagonal): key j is masked
-// for query i < j, and key blocks past the workgroup's last query are skipped.
-template <typename T, bool CAUSAL = false>
-__global__ __launch_bounds__(256) void attention_kernel(const u16* __restrict__ qkv,
-                                                        u16* __restrict__ out, int N, int H) {
-    typedef typename T::vec8 vec8;
-    __shared__ __attribute__((aligned(16))) unsigned char smem[64 * 128 * 2];
-    unsigned char* Ks = smem;             // [64 keys][64 d]
-    unsigned char* Vt = smem + 64 * 128;  // [64 d][64 keys]
-
-    const int D = H * 64;
-    const int ld = 3 * D;
-    const int qb = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int j = lane & 15, g = lane >> 4;
-    const size_t base = (size_t)b * N;
-
-    // Q fragments (B operand of S^T): lane holds Q[q][32 s + 8 g .. +7]
-    const int q = qb * 64 + wave * 16 + j;
-    const int qc = min(q, N - 1);
-    const u16* qrow = qkv + (base + qc) * ld + h * 64;
-    vec8 qf[2];
-    qf[0] = *(const vec8*)(qrow + 8 * g);
-    qf[1] = *(const vec8*)(qrow + 32 + 8 * g);
-
-    f32x4 o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY, l_run = 0.f;
-    const float scale = 0.125f;  // 1/sqrt(64)
-
-    const int nkb = CAUSAL ? min((N + 63) >> 6, qb + 1) : (N + 63) >> 6;
-    for (int kb = 0; kb < nkb; ++kb) {
-        __syncthreads();
-        {   // cooperative load of 64 keys: thread -> (key = tid>>2, d = 16*(tid&3) .. +15)
-            const int key = tid >> 2, dq = (tid & 3) * 16;
-            const int kg = kb * 64 + key;
-            uint4 k0 = make_uint4(0, 0, 0, 0), k1 = k0, v0 = k0, v1 = k0;
-            if (kg < N) {
-                const u16* kr = qkv + (base + kg) * ld + D + h * 64 + dq;
-                const u16* vr = kr + D;
-                k0 = *(const uint4*)kr; k1 = *(const uint4*)(kr + 8);
-                v0 = *(const uint4*)vr; v1 = *(const uint4*)(vr + 8);
-            }
-            const int c0 = dq >> 3;
-            *(uint4*)(Ks + key * 128 + (((c0) ^ (key & 7)) << 4)) = k0;
-            *(uint4*)(Ks + key * 128 + (((c0 + 1) ^ (key & 7)) << 4)) = k1;
-            const u16* vv0 = (const u16*)&v0;
-            const u16* vv1 = (const u16*)&v1;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int d = dq + i;
-                const u16 val = i < 8 ? vv0[i] : vv1[i - 8];
-                const int ch = (key >> 2) ^ (((d >> 1) & 7) << 1);
-                *(u16*)(Vt + d * 128 + (ch << 3) + (key & 3) * 2) = val;
-            }
-        }
-        __syncthreads();
-
-        // S^T = K Q^T  (4 key subtiles x 2 d-steps)
-        f32x4 s[4];
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int row = kt * 16 + j;
-#pragma unroll
-            for (int ds = 0; ds < 2; ++ds) {
-                const int c = ((ds << 2) | g) ^ (row & 7);
-                const vec8 kf = *(const vec8*)(Ks + row * 128 + (c << 4));
-                s[kt] = T::mfma16(kf, qf[ds], s[kt]);
-            }
-        }
-        // scale, mask, block max: lane holds keys kb*64 + 16 kt + 4 g + r
-        float mloc = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int key = kb * 64 + kt * 16 + 4 * g + r;
-                const bool live = key < N && (!CAUSAL || key <= q);
-                const float v = live ? s[kt][r] * scale : -INFINITY;
-                s[kt][r] = v;
-                mloc = fmaxf(mloc, v);
-            }
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
-        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
-        const float m_new = fmaxf(m_run, mloc);
-        const float alpha = __expf(m_run - m_new);
-        m_run = m_new;
-        float lsum = 0.f;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float p = __expf(s[kt][r] - m_new);
-                s[kt][r] = p;
-                lsum += p;
-            }
-        l_run = l_run * alpha + lsum;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] *= alpha;
-
-        // O^T += V^T P^T over two 32-key steps; k-slot (g, e) <-> key 32 st + 16 (e>>2) + 4 g + (e&3)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            vec8 pf;
-            {
-                unsigned w[4] = {pack2<T>(s[2 * st][0], s[2 * st][1]), pack2<T>(s[2 * st][2], s[2 * st][3]),
-                                 pack2<T>(s[2 * st + 1][0], s[2 * st + 1][1]),
-                                 pack2<T>(s[2 * st + 1][2], s[2 * st + 1][3])};
-                pf = __builtin_bit_cast(vec8, *(uint4*)w);
-            }
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                const int d = dt * 16 + j;
-                const int sw = ((d >> 1) & 7) << 1;
-                const int ch0 = (8 * st + g) ^ sw;       // keys 32 st + 4 g .. +3
-                const int ch1 = (8 * st + 4 + g) ^ sw;   // keys 32 st + 16 + 4 g .. +3
-                const uint2 lo = *(const uint2*)(Vt + d * 128 + (ch0 << 3));
-                const uint2 hi = *(const uint2*)(Vt + d * 128 + (ch1 << 3));
-                const uint4 vv = make_uint4(lo.x, lo.y, hi.x, hi.y);
-                o[dt] = T::mfma16(__builtin_bit_cast(vec8, vv), pf, o[dt]);
-            }
-        }
-    }
-
-    // finish: total row sum over the 4 lanes of the query, normalise, store O[q][16 dt + 4 g + r]
-    l_run += __shfl_xor(l_run, 16, 64);
-    l_run += __shfl_xor(l_run, 32, 64);
-    if (q < N) {
-        const float inv = 1.0f / l_run;
-        u16* orow = out + (base + q) * D + h * 64;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            uint2 w;
-            w.x = pack2<T>(o[dt][0] * inv, o[dt][1] * inv);
-            w.y = pack2<T>(o[dt][2] * inv, o[dt][3] * inv);
-            *(uint2*)(orow + dt * 16 + 4 * g) = w;
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------------------
-// attention_v2_kernel (non-causal, the vision tower's default): same math and register
-// layout as attention_kernel, but K and V blocks reach LDS by global_load_lds (async, no VGPR
-// staging) into a 2-stage ring, so block kb+1 streams in while block kb is computed, and V is
-// stored row-major exactly like K (16-B chunk c ^ (key & 7)) and read TRANSPOSED by
-// ds_read_b64_tr_b16: lane group g, lane 4q + p supplies key r0 + q, columns 4p .. 4p + 3;
-// lane i receives column d = 16 dt + i of the 4 keys — the A operand of O^T += V^T P^T with
-// the k order of P (k-slot (g, e) <-> key 32 st + 16 (e >> 2) + 4 g + (e & 3)). No scalar
-// LDS transposes, no __syncthreads (raw s_barrier + counted vmcnt keep the next block's loads
-// in flight). Key rows past the sequence read as zeros (outside the rebased buffer range) and
-// are masked to -inf in S.
+// attention_v2_kernel (the vision tower at N <= 128, and the causal text tower): K and V blocks
+// reach LDS by buffer loads straight into LDS (async, no VGPR staging) into a 2-stage ring, so
+// block kb+1 streams in while block kb is computed. V is stored row-major exactly like K (16-B
+// chunk c ^ (key & 7)) and read TRANSPOSED by ds_read_b64_tr_b16: lane group g, lane 4q + p
+// supplies key r0 + q, columns 4p .. 4p + 3; lane i receives column d = 16 dt + i of the 4
+// keys — the A operand of O^T += V^T P^T with the k order of P (k-slot (g, e) <-> key
+// 32 st + 16 (e >> 2) + 4 g + (e & 3)). No scalar LDS transposes, no __syncthreads (raw
+// s_barrier + counted vmcnt keep the next block's loads in flight). Key rows past the sequence
+// read as zeros (outside the rebased buffer range) and are masked to -inf in S.
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 // QW waves per workgroup = 16 QW queries; every wave loads 64 / QW key rows of K and of V
-// per block (QW = 8 halves the K/V re-reads of long sequences: the fill path bounds them).
+// per block (long sequences run attention_v3_kernel instead, which halves the LDS reads).
 // SINGLE (N <= 64, the B/32 shape): one key block, one LDS stage, no loop state — fewer live
 // registers, so more workgroups per CU hide the load latency.
 // CAUSAL (text tower): key j masked for query i < j; key blocks past the workgroup's last query
@@ -574,16 +430,15 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
 }
 
 // kernel choice by sequence length: attention_v3 (two query fragments per wave) for N > 128,
-// attention_v2 (one key block, ViT-B/32's N = 50) for N <= 64
-static constexpr int attn_v3() { return 1; }  // 1: long sequences only (2 = also N <= 64, measured slower)
-static constexpr bool attn_v2() { return true; }
+// attention_v2 for N <= 128 (one key block at N <= 64: ViT-B/32's N = 50) and for the causal
+// text tower. Two query fragments per wave at N <= 64 measured slower.
 
 // attention with the output quantized to MX-fp8 (q8 [B N, D] e4m3 + q8s [B N, D / 32] scales) in
 // the kernel, for the shapes that run on the one-key-block attention_v2 (N <= 64: ViT-B/32);
 // returns -1 otherwise (the caller then runs launch_attention + launch_quant_mx8, the same bytes)
 int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,
                         int B, int N, int H) {
-    if (!attn_v2() || N > 64 || attn_v3() >= 2) return -1;
+    if (N > 64) return -1;
     dim3 grid(1, H, B), block(256);
     const u16* in = (const u16*)qkv;
     if (dtype == 2) attention_v2_kernel<F16, 4, true, false, true><<<grid, block, 0, s>>>(in, nullptr, N, H, q8, q8s);
@@ -594,47 +449,21 @@ int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
                       bool causal) {
     dim3 grid((N + 63) / 64, H, B), block(256);
-    if (causal && attn_v2()) {  // text tower: the glds-ring kernel with the causal mask
-        if (dtype == 2)
-            attention_v2_kernel<F16, 4, false, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v2_kernel<BF16, 4, false, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (causal) {
-        if (dtype == 2)
-            attention_kernel<F16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_kernel<BF16, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v3() >= 1 && N > 128) {  // long sequences: 4 waves x 32 queries
+    const u16* in = (const u16*)qkv;
+    u16* o = (u16*)out;
+    if (causal) {  // text tower: key blocks past the workgroup's last query are skipped
+        if (dtype == 2) attention_v2_kernel<F16, 4, false, true><<<grid, block, 0, s>>>(in, o, N, H);
+        else attention_v2_kernel<BF16, 4, false, true><<<grid, block, 0, s>>>(in, o, N, H);
+    } else if (N > 128) {  // long sequences: 4 waves x 32 queries
         dim3 g4((N + 127) / 128, H, B);
-        if (dtype == 2)
-            attention_v3_kernel<F16, 4><<<g4, 256, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v3_kernel<BF16, 4><<<g4, 256, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v3() >= 2 && N <= 64) {  // one key block: 2 waves x 32 queries
-        if (dtype == 2)
-            attention_v3_kernel<F16, 2, true><<<grid, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v3_kernel<BF16, 2, true><<<grid, 128, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v2() && N > 128) {  // long sequences: 128 queries per workgroup
-        dim3 g8((N + 127) / 128, H, B);
-        if (dtype == 2)
-            attention_v2_kernel<F16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v2_kernel<BF16, 8><<<g8, 512, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v2() && N <= 64) {
-        if (dtype == 2)
-            attention_v2_kernel<F16, 4, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v2_kernel<BF16, 4, true><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (attn_v2()) {
-        if (dtype == 2)
-            attention_v2_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-        else
-            attention_v2_kernel<BF16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
-    } else if (dtype == 2) {
-        attention_kernel<F16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        if (dtype == 2) attention_v3_kernel<F16, 4><<<g4, 256, 0, s>>>(in, o, N, H);
+        else attention_v3_kernel<BF16, 4><<<g4, 256, 0, s>>>(in, o, N, H);
+    } else if (N <= 64) {  // one key block, one LDS stage
+        if (dtype == 2) attention_v2_kernel<F16, 4, true><<<grid, block, 0, s>>>(in, o, N, H);
+        else attention_v2_kernel<BF16, 4, true><<<grid, block, 0, s>>>(in, o, N, H);
     } else {
-        attention_kernel<BF16><<<grid, block, 0, s>>>((const u16*)qkv, (u16*)out, N, H);
+        if (dtype == 2) attention_v2_kernel<F16><<<grid, block, 0, s>>>(in, o, N, H);
+        else attention_v2_kernel<BF16><<<grid, block, 0, s>>>(in, o, N, H);
     }
 }
 
