@@ -219,6 +219,9 @@ struct clipvit_handle {
     unsigned long long calls = 0;  // acquire_ws counter (workspace LRU)
     int max_inflight = 2;  // workspaces kept for calls in flight on different streams (tuning max_inflight)
     int tail_var = 90;  // GEMM tile of the class-token tail (64x64, 4-stage ring; tuning tail_variant)
+    // split-K of the class-token tail's GEMMs: the most slices (<= tail_smax, dividing K / 64)
+    // that leave every slice >= tail_kmin deep (tuning tail_kmin / tail_smax)
+    int tail_kmin = 192, tail_smax = 8;
     // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
     // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
     // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
@@ -611,7 +614,7 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     u16* hc = (u16*)(base + (size_t)B * D * 4);
     u16* uc = hc + (size_t)B * D;
     // split-K partial products: the full-M qkv buffer is dead once gather_cls has run
-    // (S * B * 4D * 4 bytes <= B * N * 3D * 2 for S <= 8, N >= 50)
+    // (S * B * n * 4 bytes <= B * N * 3D * 2 bounds S per GEMM: 18 slices for c_fc at N = 50)
     float* part = (float*)w->qkv;
     launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D, x16, x24);
     // M = B rows: 64x64 tiles alone give B/64 x N/64 workgroups whose K-long dependency chains
@@ -620,8 +623,10 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     // Measured tail 0.064 ms with one K chain (c_proj alone 27 us).
     auto g0 = [&](const void* A, const void* W, int n, int k, int& S) {
         S = 1;
-        for (int c : {8, 4, 2})
-            if (k % (64 * c) == 0 && k / c >= 192) { S = c; break; }
+        const int nkt = k / 64;
+        const long cap = (long)N * 3 * D * 2 / ((long)n * 4);  // slices the dead qkv buffer holds
+        for (int c = std::min(h->tail_smax, nkt); c >= 2; --c)
+            if (nkt % c == 0 && k / c >= h->tail_kmin && c <= cap) { S = c; break; }
         GemmArgs a{};
         a.A = A; a.W = W; a.bias = nullptr; a.C = part;
         a.M = B; a.N = n; a.K = k; a.ldc = n; a.ksplit = S;
@@ -1116,6 +1121,8 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
+    else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
+    else if (k == "tail_smax") ok = parse_int(v, h->tail_smax) && h->tail_smax >= 1 && h->tail_smax <= 48;
     else if (k == "split_xcd") ok = parse_int(v, h->split_xcd);
     else if (k == "max_inflight") {
         ok = parse_int(v, x) && x >= 1;
@@ -1163,14 +1170,15 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
-        int split_main, split_tail, tail_var, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int split_main, split_tail, tail_var, tail_kmin, tail_smax, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
         unsigned sk_roles;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->split_xcd, g->max_inflight,
+              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax,
+              g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
@@ -1186,6 +1194,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
+            h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
             h->mx8_split_tail = before.mx8_split_tail;
             memcpy(h->xcd, before.xcd, sizeof before.xcd);

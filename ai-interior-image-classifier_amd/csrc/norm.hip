@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void splitk_resid_ln_kernel(float* __restrict_
         v[i] = *(const float4*)(xr + (lane + 64 * i) * 4);
         t[i] = *(const float4*)(pr + (lane + 64 * i) * 4);
     }
-    for (int z = 1; z < S; ++z) {
+#pragma unroll 4
+    for (int z = 1; z < S; ++z) {  // unrolled: the slices' loads issue together, adds in slice order
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             const float4 q = *(const float4*)(pr + z * ps + (lane + 64 * i) * 4);
@@ -430,6 +431,7 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
     if (i4 * 4 >= tot) return;
     const size_t e = i4 * 4;
     float4 t = *(const float4*)(P + e);
+#pragma unroll 4
     for (int z = 1; z < S; ++z) {
         const float4 q = *(const float4*)(P + z * tot + e);
         t.x += q.x; t.y += q.y; t.z += q.z; t.w += q.w;
