@@ -222,6 +222,10 @@ struct clipvit_handle {
     // split-K of the class-token tail's GEMMs: the most slices (<= tail_smax, dividing K / 64)
     // that leave every slice >= tail_kmin deep (tuning tail_kmin / tail_smax)
     int tail_kmin = 192, tail_smax = 8;
+    // output columns per workgroup of the head products (tuning head_cols 64 / 32, bit-identical):
+    // 32 doubles the workgroups of ln_post @ proj (128 -> 256 at bs 256); head family 0.020 ->
+    // 0.018-0.019 ms per forward, 3 alternations on one box (profiles/ablog.md)
+    int head_cols = 32;
     // whole-round row split of c_fc (gemm()): the persistent ping-pong tile on the rows that fill
     // whole rounds, the 128x128 tile on the rest. r03, same box: B/32 82.0k / 82.1k -> 82.9k /
     // 83.0k img/s (c_fc 0.83 -> 0.80 ms per forward)
@@ -647,7 +651,7 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     if ((rc = g0(uc, ly.wproj, D, 4 * D, S))) return rc;
     launch_splitk_resid_ln(s, h->dt, xc, part, S, ly.bproj, nullptr, nullptr, nullptr, B, D);
     if (prof) prof->mark(s, F_TAIL);
-    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E);
+    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E, h->head_cols);
     if (prof) prof->mark(s, F_HEAD);
     return 0;
 }
@@ -736,7 +740,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
             if (prof) prof->mark(s, F_LN);
         }
     }
-    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E, h->head_cols);
     if (prof) prof->mark(s, F_HEAD);
     HIPCHK(hipGetLastError());
     return 0;
@@ -780,7 +784,7 @@ static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float
     if (prof) prof->mark(s, F_TAIL);
     if ((rc = g0(EPI_RESID, h->tail_var, uc, ly.wproj, ly.bproj, xc, D, 4 * D, Fold()))) return rc;
     if (prof) prof->mark(s, F_TAIL);
-    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E);
+    launch_cls_ln_proj(s, xc, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, 1, D, h->E, h->head_cols);
     if (prof) prof->mark(s, F_HEAD);
     return 0;
 }
@@ -829,7 +833,7 @@ static int forward_fold(clipvit_handle* h, hipStream_t s, const void* pix, int i
         if ((rc = gemm(s, h, EPI_RES_STATS, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ, fp))) return rc;
         if (prof) prof->mark(s, F_PROJ);
     }
-    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E, h->head_cols);
     if (prof) prof->mark(s, F_HEAD);
     HIPCHK(hipGetLastError());
     return 0;
@@ -904,7 +908,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             }
         }
     }
-    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E);
+    launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E, h->head_cols);
     if (prof) prof->mark(s, F_HEAD);
     HIPCHK(hipGetLastError());
     return 0;
@@ -1122,6 +1126,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
+    else if (k == "head_cols") ok = parse_int(v, h->head_cols) && (h->head_cols == 64 || h->head_cols == 32);
     else if (k == "tail_smax") ok = parse_int(v, h->tail_smax) && h->tail_smax >= 1 && h->tail_smax <= 48;
     else if (k == "split_xcd") ok = parse_int(v, h->split_xcd);
     else if (k == "max_inflight") {
@@ -1170,14 +1175,14 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
-        int split_main, split_tail, tail_var, tail_kmin, tail_smax, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
         unsigned sk_roles;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax,
+              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1194,7 +1199,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
-            h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax;
+            h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
             h->mx8_split_tail = before.mx8_split_tail;
             memcpy(h->xcd, before.xcd, sizeof before.xcd);
@@ -1428,7 +1433,7 @@ int clipvit_classify(clipvit_handle* h, void* stream, const void* pixels_dev, in
         int r = forward(h, st, (const char*)pixels_dev + off * pxb, dtype, cnt, l, l->f, nullptr);
         if (r) return r;
         launch_logits(st, l->f, h->Tt, emb_dev ? emb_dev + off * E : nullptr, logits_dev + off * C, cnt, h->E,
-                      h->C, h->Cpad);
+                      h->C, h->Cpad, h->head_cols);
         if (probs_dev || top_idx || top_prob)
             launch_seg_softmax_topk(st, logits_dev + off * C, probs_dev ? probs_dev + off * C : nullptr,
                                     top_idx ? top_idx + off * T5 : nullptr,

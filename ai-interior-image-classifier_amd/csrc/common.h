@@ -391,9 +391,9 @@ void launch_fill_random16(hipStream_t s, int dtype, void* p, size_t n, unsigned 
 void launch_lora_merge(hipStream_t s, float* W, const float* A, const float* Bm, int in_f,
                        int out_f, int rank, float scaling);
 void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,
-                        const float* proj, float* f, int B, int N, int D, int E);
+                        const float* proj, float* f, int B, int N, int D, int E, int tc = 64);
 void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_norm, float* logits,
-                   int B, int E, int C, int Cpad);
+                   int B, int E, int C, int Cpad, int tc = 64);
 void launch_seg_softmax_topk(hipStream_t s, const float* logits, float* probs, int* top_idx,
                              float* top_prob, const int* seg_off, int nseg, int B, int C);
 

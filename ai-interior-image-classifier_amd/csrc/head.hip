@@ -92,62 +92,80 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ src, size_t
     }
 }
 
-// P = xs[16][K] @ W[K][col0 .. col0 + 64)  (K % 128 == 0), xs in LDS (row stride K + 4) staged
-// by `stage()`, which runs while the first two weight chunks are in flight. Weight chunks
-// (128 x 64) go global -> registers two chunks ahead of the multiply, registers -> LDS ws. Wave
-// w multiplies k-rows [16 w, 16 w + 16) of every chunk into a full 16 x 64 partial tile (lane:
-// images 4 (lane >> 4) .. + 3, columns 4 (lane & 15) .. + 3); the HW partials are summed in a
-// fixed order at the end. On return, threads tid < 256 hold in red[i] the output (image tid >> 4,
-// columns 4 (tid & 15) + i).
-template <typename Stage>
+// P = xs[16][K] @ W[K][col0 .. col0 + TC)  (K % 128 == 0; TC = 64 or 32 output columns per
+// workgroup), xs in LDS (row stride K + 4) staged by `stage()`, which runs while the first two
+// weight chunks are in flight. Weight chunks (128 x TC) go global -> registers two chunks ahead
+// of the multiply, registers -> LDS ws (row stride TC + 4). Wave w multiplies k-rows
+// [16 w, 16 w + 16) of every chunk into a full 16 x TC partial tile (lane: images 4 (lane >> 4)
+// .. + 3, columns CPL (lane & 15) .. + CPL - 1, CPL = TC / 16); the HW partials are summed in a
+// fixed order at the end. On return, threads tid < 4 TC hold in red[i] the output (image
+// tid / (TC / 4), columns 4 (tid % (TC / 4)) + i). Every output element sees the same
+// arithmetic in the same order for either TC (bit-identical results).
+template <int TC, typename Stage>
 __device__ __forceinline__ void tile_product(const float* xs, int K, const float* __restrict__ W, int ldw,
                                              int col0, float* ws, float (&red)[4], int tid, Stage&& stage) {
-    constexpr int KW = HK / HW;  // k-rows of a chunk per wave
+    constexpr int KW = HK / HW;      // k-rows of a chunk per wave
+    constexpr int CPL = TC / 16;     // output columns per lane
+    constexpr int TPR = TC / 4;      // threads per weight row (one float4 each)
+    constexpr int RPP = HT / TPR;    // weight rows per load pass
+    constexpr int NP = HK / RPP;     // load passes per chunk (4 for TC = 64, 2 for 32)
+    constexpr int WS = TC + 4;       // ws row stride (floats)
+    static_assert(TC == 64 || TC == 32, "column tile");
     const int lane = tid & 63, wave = tid >> 6;
     const int ig = lane >> 4, cg = lane & 15;
-    const int lr = tid >> 4, lc = (tid & 15) * 4;  // lr < HT / 16 = 32
+    const int lr = tid / TPR, lc = (tid % TPR) * 4;
     const int nc = K / HK;
     const int xstride = K + 4;
-    float acc[4][4] = {};
-    // two register chunks of 4 float4 (named scalars: an array here ends up in scratch)
+    float acc[4][CPL] = {};
+    // two register chunks of NP float4 (named scalars: an array here ends up in scratch)
     float4 a0, a1, a2, a3, b0, b1, b2, b3;
-    const size_t l32 = (size_t)32 * ldw;
+    const size_t lpass = (size_t)RPP * ldw;
 #define HEAD_LOAD(x0, x1, x2, x3, k0)                                      \
     {                                                                      \
         const float* p_ = W + (size_t)((k0) + lr) * ldw + col0 + lc;       \
         x0 = *(const float4*)p_;                                           \
-        x1 = *(const float4*)(p_ + l32);                                   \
-        x2 = *(const float4*)(p_ + 2 * l32);                               \
-        x3 = *(const float4*)(p_ + 3 * l32);                               \
+        x1 = *(const float4*)(p_ + lpass);                                 \
+        if constexpr (NP == 4) {                                           \
+            x2 = *(const float4*)(p_ + 2 * lpass);                         \
+            x3 = *(const float4*)(p_ + 3 * lpass);                         \
+        }                                                                  \
     }
 #define HEAD_PUT(x0, x1, x2, x3)                                           \
     {                                                                      \
-        float* q_ = ws + lr * 68 + lc;                                     \
+        float* q_ = ws + lr * WS + lc;                                     \
         *(float4*)q_ = x0;                                                 \
-        *(float4*)(q_ + 32 * 68) = x1;                                     \
-        *(float4*)(q_ + 64 * 68) = x2;                                     \
-        *(float4*)(q_ + 96 * 68) = x3;                                     \
+        *(float4*)(q_ + RPP * WS) = x1;                                    \
+        if constexpr (NP == 4) {                                           \
+            *(float4*)(q_ + 2 * RPP * WS) = x2;                            \
+            *(float4*)(q_ + 3 * RPP * WS) = x3;                            \
+        }                                                                  \
     }
     auto mul = [&](int k0) {
         const float* xr = xs + (4 * ig) * xstride + k0 + KW * wave;
-        const float* wr = ws + (KW * wave) * 68 + 4 * cg;
+        const float* wr = ws + (KW * wave) * WS + CPL * cg;
 #pragma unroll
         for (int k = 0; k < KW; k += 4) {
-            float4 x[4], w[4];
+            float4 x[4];
+            float w[4][CPL];
 #pragma unroll
             for (int i = 0; i < 4; ++i) x[i] = *(const float4*)(xr + i * xstride + k);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) w[j] = *(const float4*)(wr + (k + j) * 68);
+            for (int j = 0; j < 4; ++j) {
+                if constexpr (CPL == 4) {
+                    const float4 t = *(const float4*)(wr + (k + j) * WS);
+                    w[j][0] = t.x; w[j][1] = t.y; w[j][2] = t.z; w[j][3] = t.w;
+                } else {
+                    const float2 t = *(const float2*)(wr + (k + j) * WS);
+                    w[j][0] = t.x; w[j][1] = t.y;
+                }
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    acc[i][0] += xv[j] * w[j].x;
-                    acc[i][1] += xv[j] * w[j].y;
-                    acc[i][2] += xv[j] * w[j].z;
-                    acc[i][3] += xv[j] * w[j].w;
-                }
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) acc[i][c] += xv[j] * w[j][c];
             }
         }
     };
@@ -171,60 +189,62 @@ __device__ __forceinline__ void tile_product(const float* xs, int K, const float
 #undef HEAD_PUT
     // sum the HW per-wave partial tiles (fixed order) through LDS
     __syncthreads();
-    float* part = ws;  // [HW waves][16 images][64 columns]
+    float* part = ws;  // [HW waves][16 images][TC columns]
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        *(float4*)(part + wave * 1024 + (4 * ig + i) * 64 + 4 * cg) =
-            make_float4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c) part[wave * 16 * TC + (4 * ig + i) * TC + CPL * cg + c] = acc[i][c];
     __syncthreads();
-    const int img = (tid & 255) >> 4, cq = (tid & 15) * 4;
+    const int img = (tid / TPR) & 15, cq = (tid % TPR) * 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[i] = 0.f;
 #pragma unroll
     for (int w = 0; w < HW; ++w) {
-        const float4 v = *(const float4*)(part + w * 1024 + img * 64 + cq);
+        const float4 v = *(const float4*)(part + w * 16 * TC + img * TC + cq);
         red[0] += v.x; red[1] += v.y; red[2] += v.z; red[3] += v.w;
     }
 }
 
-// grid (ceil(B/16), E/64), HT threads.
+// grid (ceil(B/16), E/TC), HT threads.
+template <int TC>
 __global__ __launch_bounds__(HT) void cls_ln_proj_kernel(const float* __restrict__ x,
                                                           const float* __restrict__ gm,
                                                           const float* __restrict__ bt,
                                                           const float* __restrict__ proj,
                                                           float* __restrict__ f, int B, int N,
                                                           int D, int E) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][D] + [128][68]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][D + 4] + [128][TC + 4]
     float* ys = sm;
     float* ws = sm + HR * (D + 4);
     const int tid = threadIdx.x;
-    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * 64;
+    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * TC;
     float red[4];
-    tile_product(ys, D, proj, E, col0, ws, red, tid, [&]() {  // CLS token = row 0 of each image
+    tile_product<TC>(ys, D, proj, E, col0, ws, red, tid, [&]() {  // CLS token = row 0 of each image
         stage_rows<0>(x, (size_t)N * D, b0, B, D, gm, bt, ys, nullptr);
     });
-    const int b = b0 + (tid >> 4);
-    if (tid < 256 && b < B)
-        *(float4*)(f + (size_t)b * E + col0 + (tid & 15) * 4) = make_float4(red[0], red[1], red[2], red[3]);
+    const int b = b0 + tid / (TC / 4);
+    if (tid < 4 * TC && b < B)
+        *(float4*)(f + (size_t)b * E + col0 + (tid % (TC / 4)) * 4) = make_float4(red[0], red[1], red[2], red[3]);
 }
 
-// grid (ceil(B/16), Cpad/64), HT threads.
+// grid (ceil(B/16), Cpad/TC), HT threads.
+template <int TC>
 __global__ __launch_bounds__(HT) void logits_kernel(const float* __restrict__ f,
                                                      const float* __restrict__ Tt,
                                                      float* __restrict__ emb_norm,
                                                      float* __restrict__ logits, int B, int E,
                                                      int C, int Cpad) {
-    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][E] + [128][68]
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // [16][E + 4] + [128][TC + 4]
     float* fs = sm;
     float* ws = sm + HR * (E + 4);
     const int tid = threadIdx.x;
-    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * 64;
+    const int b0 = blockIdx.x * HR, col0 = blockIdx.y * TC;
     float red[4];
-    tile_product(fs, E, Tt, Cpad, col0, ws, red, tid, [&]() {
+    tile_product<TC>(fs, E, Tt, Cpad, col0, ws, red, tid, [&]() {
         stage_rows<1>(f, (size_t)E, b0, B, E, nullptr, nullptr, fs, blockIdx.y == 0 ? emb_norm : nullptr);
     });
-    const int b = b0 + (tid >> 4), c = col0 + (tid & 15) * 4;
-    if (tid < 256 && b < B) {
+    const int b = b0 + tid / (TC / 4), c = col0 + (tid % (TC / 4)) * 4;
+    if (tid < 4 * TC && b < B) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
             if (c + i < C) logits[(size_t)b * C + c + i] = 100.0f * red[i];
@@ -286,26 +306,42 @@ __global__ __launch_bounds__(64 * SM_WAVES) void seg_softmax_topk_kernel(
     }
 }
 
-void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,
-                        const float* proj, float* f, int B, int N, int D, int E) {
-    static const bool attr = hipFuncSetAttribute((const void*)cls_ln_proj_kernel,
+template <int TC>
+static void cls_ln_proj_t(hipStream_t s, const float* x, const float* g, const float* b, const float* proj,
+                          float* f, int B, int N, int D, int E) {
+    static const bool attr = hipFuncSetAttribute((const void*)cls_ln_proj_kernel<TC>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  160 * 1024) == hipSuccess;
     (void)attr;
-    dim3 grid((B + HR - 1) / HR, E / 64), block(HT);
-    const size_t lds = (HR * (D + 4) + HK * 68) * sizeof(float);
-    cls_ln_proj_kernel<<<grid, block, lds, s>>>(x, g, b, proj, f, B, N, D, E);
+    dim3 grid((B + HR - 1) / HR, E / TC), block(HT);
+    const size_t lds = (HR * (D + 4) + HK * (TC + 4)) * sizeof(float);
+    cls_ln_proj_kernel<TC><<<grid, block, lds, s>>>(x, g, b, proj, f, B, N, D, E);
+}
+
+template <int TC>
+static void logits_t(hipStream_t s, const float* f, const float* Tt, float* emb_norm, float* logits, int B,
+                     int E, int C, int Cpad) {
+    static const bool attr = hipFuncSetAttribute((const void*)logits_kernel<TC>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024) == hipSuccess;
+    (void)attr;
+    dim3 grid((B + HR - 1) / HR, Cpad / TC), block(HT);
+    const size_t lds = (HR * (E + 4) + HK * (TC + 4)) * sizeof(float);
+    logits_kernel<TC><<<grid, block, lds, s>>>(f, Tt, emb_norm, logits, B, E, C, Cpad);
+}
+
+// tc = output columns per workgroup (64 or 32; 32 doubles the workgroups of the small-batch
+// grids, the arithmetic per output element is the same)
+void launch_cls_ln_proj(hipStream_t s, const float* x, const float* g, const float* b,
+                        const float* proj, float* f, int B, int N, int D, int E, int tc) {
+    if (tc == 32) cls_ln_proj_t<32>(s, x, g, b, proj, f, B, N, D, E);
+    else cls_ln_proj_t<64>(s, x, g, b, proj, f, B, N, D, E);
 }
 
 void launch_logits(hipStream_t s, const float* f, const float* Tt, float* emb_norm, float* logits,
-                   int B, int E, int C, int Cpad) {
-    static const bool attr = hipFuncSetAttribute((const void*)logits_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 160 * 1024) == hipSuccess;
-    (void)attr;
-    dim3 grid((B + HR - 1) / HR, Cpad / 64), block(HT);
-    const size_t lds = (HR * (E + 4) + HK * 68) * sizeof(float);
-    logits_kernel<<<grid, block, lds, s>>>(f, Tt, emb_norm, logits, B, E, C, Cpad);
+                   int B, int E, int C, int Cpad, int tc) {
+    if (tc == 32) logits_t<32>(s, f, Tt, emb_norm, logits, B, E, C, Cpad);
+    else logits_t<64>(s, f, Tt, emb_norm, logits, B, E, C, Cpad);
 }
 
 void launch_seg_softmax_topk(hipStream_t s, const float* logits, float* probs, int* top_idx,

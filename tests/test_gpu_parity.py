@@ -154,6 +154,29 @@ def test_two_lane_split_is_bit_identical(gpu):
     assert torch.equal(outs[0][2], outs[1][2])
 
 
+def test_head_column_tile_is_bit_identical(gpu):
+    """The head products (ln_post @ proj, 100 f_hat T^T) on 32-column workgroups (tuning
+    head_cols=32) do every output element's arithmetic in the same order as on 64-column ones:
+    features, logits, probabilities and top-k equal bit for bit (B = 67: a ragged 16-image group)."""
+    cfg = C.VIT_B32
+    sd = synthetic_state_dict(cfg, 0)
+    T = _text(cfg.embed_dim, 437)
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    px = _pixels(67, 224, seed=29).to(gpu)
+    outs = []
+    for cols in ("64", "32"):
+        eng = VisionEngine(cfg, 0, "fp16", max_batch=67, tuning={"head_cols": cols})
+        eng.load_state_dict(sd)
+        eng.set_text_features(T.numpy(), seg)
+        o = eng.classify(px)
+        torch.cuda.synchronize()
+        outs.append((o.logits.clone(), o.probs.clone(), o.top_idx.clone(), o.emb.clone(),
+                     eng.encode_image(px).clone()))
+        eng.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
 def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, dtype):
