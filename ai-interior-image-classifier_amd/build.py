@@ -3,7 +3,7 @@
 Compiles every ``csrc/*.hip`` translation unit with ``hipcc --offload-arch=gfx950`` in
 parallel and links them into ``libclipvit_hip.so`` next to this file, so the shared library
 travels with the repository snapshot to the GPU box. Incremental: a unit is recompiled only
-when it, ``csrc/common.h`` or ``include/clipvit.h`` is newer than its object file.
+when it, a ``csrc/*.h`` header or ``include/clipvit.h`` is newer than its object file.
 """
 from __future__ import annotations
 
@@ -47,7 +47,7 @@ def _needs(obj: Path, deps: list[Path]) -> bool:
 
 def _compile(src: Path) -> tuple[Path, str]:
     obj = BUILD / (src.stem + ".o")
-    deps = [src, CSRC / "common.h", INCLUDE / "clipvit.h", Path(__file__)]  # this file: the flags
+    deps = [src, *CSRC.glob("*.h"), INCLUDE / "clipvit.h", Path(__file__)]  # this file: the flags
     if not _needs(obj, deps):
         return obj, ""
     cmd = [HIPCC, *CFLAGS, *SRC_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)]

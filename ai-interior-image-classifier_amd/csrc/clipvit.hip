@@ -77,12 +77,6 @@ struct Lane {
     float2* st = nullptr;  // lnfold: [cap*N, D/128] per-row 128-column (mean, M2) of x
     unsigned char* q8 = nullptr;  // MX-fp8 mode: [cap*N, D] e4m3 GEMM operand + [cap*N, D/32] scales
     void* x16 = nullptr;  // MX-fp8 mode: [cap*N, D] fp16 residual stream (handle x16)
-    // stream-K GEMM workspace (gemm_pp.hip variant 65): fp32 partial slots [ncu][256 KB] and
-    // flags [ncu + 1][8]; sk_epoch counts this lane's stream-K launches (flags equal to it are
-    // the current launch's: the lane's launches are ordered on its stream)
-    void* sk_part = nullptr;
-    unsigned* sk_flag = nullptr;
-    unsigned sk_epoch = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // recorded after the last kernel that touched the buffers
 };
@@ -253,13 +247,6 @@ struct clipvit_handle {
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
     // ms per forward, main-launch traffic 1.59x -> 1.38x of algorithmic
     int split_xcd = 34;
-    // stream-K GEMM (gemm_pp.hip variant 65) for these roles (bit = Role; tuning stream_k): one
-    // launch in which every CU owns an equal share of the k-tile iterations, in place of the
-    // whole-round row split. Off: measured 94.8 us against 77.3 (one launch) and 73.7 (row split)
-    // for c_fc at bs 256 — the shares start at different k, so workgroups that share an operand
-    // panel need its k-slices at different times and the L2 working set becomes whole panels
-    // (2.5 us per k-tile against 1.7)
-    unsigned sk_roles = 0;
     // c_fc -> c_proj intermediate u in the 16-row blocked layout (common.h blk16_off): c_fc's
     // accumulator-layout stores become 256-B runs per quarter-wave instead of 16 scattered
     // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
@@ -308,8 +295,6 @@ static int free_ws(Workspace* w) {
         hipFree(l.st);
         hipFree(l.q8);
         hipFree(l.x16);
-        hipFree(l.sk_part);
-        hipFree(l.sk_flag);
         if (l.done) hipEventDestroy(l.done);
         if (l.stream) hipStreamDestroy(l.stream);
     }
@@ -341,11 +326,6 @@ static int alloc_ws(clipvit_handle* h, Workspace** out) {
         if (e == hipSuccess && h->mx8) e = hipMalloc((void**)&l.q8, rows * h->D + rows * h->D / 32);
         if (e == hipSuccess && h->mx8) e = hipMalloc(&l.x16, rows * h->D * 2);
         else if (e == hipSuccess && h->use_x24()) e = hipMalloc(&l.x16, rows * h->D * 3);
-        if (e == hipSuccess && h->sk_roles) {
-            e = hipMalloc(&l.sk_part, (size_t)h->ncu * 256 * 256 * 4);
-            if (e == hipSuccess) e = hipMalloc((void**)&l.sk_flag, (size_t)(h->ncu + 1) * 8 * 4);
-            if (e == hipSuccess) e = hipMemset(l.sk_flag, 0, (size_t)(h->ncu + 1) * 8 * 4);
-        }
         if (e == hipSuccess) e = hipEventCreateWithFlags(&l.done, hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking);
     }
@@ -437,9 +417,9 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
-    // every R_FC output / R_PROJ input is the lane's u; forced single-buffer tiles (1-3) and
-    // stream-K cannot address the blocked layout, so those keep u row-major for both roles
-    auto blk_ok = [](int v) { return v >= 8 && v != 65; };
+    // every R_FC output / R_PROJ input is the lane's u; forced single-buffer tiles (1-3) cannot
+    // address the blocked layout, so those keep u row-major for both roles
+    auto blk_ok = [](int v) { return v >= 8; };
     const bool ublk = h->u_blk && (!h->var_forced || (blk_ok(h->var[R_FC]) && blk_ok(h->var[R_PROJ])));
     a.blk_c = ublk && role == R_FC;
     a.blk_a = ublk && role == R_PROJ;
@@ -460,20 +440,6 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the main launch's tile width: every pipelined variant a round split can use is 256 wide
     // (8 / 80: 256x256, 98: 240x256)
     const int bn = 256;
-    // stream-K: one launch, every CU the same share of k-tiles (the role's 16-bit STORE / GELU
-    // epilogue; falls through when a share would cover less than one tile's k-tiles)
-    if (lane && lane->sk_part && ((h->sk_roles >> role) & 1) && !h->var_forced && t256 &&
-        t256 >= h->ncu && t256 < 4L * h->ncu && (epi == EPI_STORE || epi == EPI_GELU)) {
-        GemmArgs b = a;
-        b.xcd_n = h->split_xcd;
-        if (xcd_split_n(N / 256, b.xcd_n)) b.xcd_n = 0;
-        b.sk_part = lane->sk_part;
-        b.sk_flag = lane->sk_flag;
-        b.sk_epoch = ++lane->sk_epoch;
-        if (b.sk_epoch == 0) b.sk_epoch = ++lane->sk_epoch;  // 0 = a never-written flag
-        if (launch_gemm(s, h->dt, epi, b, 65) == 0) return 0;
-        --lane->sk_epoch;
-    }
     // (the ping-pong main tiles, split_main >= 60, have the 16-bit STORE / GELU epilogues only:
     // the LayerNorm-fold epilogues take the single-launch path below)
     const bool split_epi = epi == EPI_STORE || epi == EPI_GELU ||
@@ -1110,11 +1076,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     bool ok = true;
     if (k == "resid16") ok = flag(h->resid16);
     else if (k == "defer_x") ok = flag(h->defer_x);
-    else if (k == "lnfold") {  // fp16 only, D <= 1024 (<= 8 statistics groups per row)
-        bool f = false;
-        ok = flag(f);
-        h->lnfold = f && h->resid16 && h->dt == CLIPVIT_F16 && h->D <= 1024;
-    } else if (k == "cls_prune") ok = flag(h->cls_prune);
+    else if (k == "lnfold") ok = flag(h->lnfold);  // resolved after every key (clipvit_set_tuning) else if (k == "cls_prune") ok = flag(h->cls_prune);
     else if (k == "round_split") ok = flag(h->round_split);
     else if (k == "attn_q8") ok = flag(h->attn_q8);
     else if (k == "x16") ok = flag(h->x16);
@@ -1143,10 +1105,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "mx8_variants") ok = parse_list(v, h->var8, 4);
     else if (k == "mx8_split_tail") ok = parse_int(v, h->mx8_split_tail) && (h->mx8_split_tail == 0 || h->mx8_split_tail == 2 || h->mx8_split_tail == 5);
     else if (k == "large_variants") ok = parse_list(v, h->large_var, 4);
-    else if (k == "stream_k") {  // role bit mask (1 QKV, 4 c_fc); 0 = off
-        ok = parse_int(v, x) && x >= 0;
-        if (ok) h->sk_roles = (unsigned)x;
-    } else if (k == "gemm_variants") {
+    else if (k == "gemm_variants") {
         ok = parse_list(v, h->var, 5);
         h->var_forced = ok;
     } else FAIL(CLIPVIT_E_INVALID, "unknown tuning key '" + k + "'");
@@ -1178,13 +1137,12 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
         int split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
-        unsigned sk_roles;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
               g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
-              g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp, g->sk_roles};
+              g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
         memcpy(t.var8, g->var8, sizeof t.var8);
         memcpy(t.large_var, g->large_var, sizeof t.large_var);
@@ -1208,10 +1166,12 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             memcpy(h->var, before.var, sizeof before.var);
             h->mx8_skip = before.mx8_skip;
             h->mx8_skip_mlp = before.mx8_skip_mlp;
-            h->sk_roles = before.sk_roles;
             return rc;
         }
     }
+    // the fold is fp16-only on the 16-bit branch path, D <= 1024 (<= 8 statistics groups per
+    // row); resolved once after every key so that the spec's key order does not matter
+    h->lnfold = h->lnfold && h->resid16 && h->dt == CLIPVIT_F16 && h->D <= 1024;
     return 0;
 }
 
@@ -1545,22 +1505,6 @@ static int current_ncu() {
     return n;
 }
 
-// stream-K workspace for the kernel-level entry points (variant 65): fresh buffers, epoch 1
-struct SkScratch {
-    void* part = nullptr;
-    unsigned* flag = nullptr;
-    ~SkScratch() {
-        if (part) (void)hipFree(part);
-        if (flag) (void)hipFree(flag);
-    }
-    int alloc(int ncu) {
-        const int n = ncu > 0 ? ncu : 256;
-        if (hipMalloc(&part, (size_t)n * 256 * 256 * 4) != hipSuccess) return -1;
-        if (hipMalloc((void**)&flag, (size_t)(n + 1) * 8 * 4) != hipSuccess) return -1;
-        return hipMemset(flag, 0, (size_t)(n + 1) * 8 * 4) == hipSuccess ? 0 : -1;
-    }
-};
-
 int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi, int variant) {
     g_err.clear();
@@ -1577,19 +1521,11 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.ncu = current_ncu();
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
-    SkScratch sk;
-    if (variant == 65) {
-        HIPCHK(hipStreamSynchronize((hipStream_t)stream));
-        if (sk.alloc(a.ncu)) FAIL(CLIPVIT_E_NOMEM, "stream-K workspace");
-        a.sk_part = sk.part;
-        a.sk_flag = sk.flag;
-        a.sk_epoch = 1;
-    }
     int rc;
-    // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 / 65 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
+    // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 65;
+                        variant == 63 || variant == 72;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;
@@ -1611,7 +1547,6 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         rc = launch_gemm(s, dtype, e, a, variant);
     }
     HIPCHK(hipFreeAsync(Wp, s));
-    if (variant == 65) HIPCHK(hipStreamSynchronize(s));  // before the workspace is freed
     if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
     HIPCHK(hipGetLastError());
     return 0;
@@ -1692,15 +1627,6 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.xcd_n = variant / 100;
     variant %= 100;
     a.ncu = current_ncu();
-    // diagnostic: persistent GEMMs on fewer workgroups (store-burst experiments)
-    if (const char* v = getenv("CLIPVIT_BENCH_GRID")) a.ncu = atoi(v);
-    SkScratch sk;
-    if (variant == 65) {
-        if (sk.alloc(a.ncu)) FAIL(CLIPVIT_E_NOMEM, "stream-K workspace");
-        a.sk_part = sk.part;
-        a.sk_flag = sk.flag;
-        a.sk_epoch = 0;
-    }
     int e = epi;  // raw Epi enum
     if (mx) {
         a.sA = (const unsigned char*)A + (size_t)M * K;
@@ -1709,7 +1635,6 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
         if (e == EPI_GELU) e = EPI_GELU_Q8;
     }
     auto launch = [&]() {
-        ++a.sk_epoch;  // stream-K: a fresh epoch per launch
         return mx ? launch_gemm_mx8(nullptr, CLIPVIT_BF16, e, a, variant) : launch_gemm(nullptr, dtype, e, a, variant);
     };
     int rc = launch();
@@ -1725,26 +1650,6 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     hipEventDestroy(t0);
     hipEventDestroy(t1);
     *avg_ms = ms / iters;
-    if (variant == 65 && !rc && getenv("CLIPVIT_SK_TRACE")) {  // diagnostic: one traced launch
-        const int G = a.ncu > 0 ? a.ncu : 256;
-        unsigned long long* tr = nullptr;
-        if (hipMalloc((void**)&tr, (size_t)G * 8 * 8) == hipSuccess) {
-            (void)hipMemset(tr, 0, (size_t)G * 8 * 8);
-            a.sk_trace = tr;
-            rc = launch();
-            std::vector<unsigned long long> t((size_t)G * 8);
-            (void)hipMemcpy(t.data(), tr, t.size() * 8, hipMemcpyDeviceToHost);
-            (void)hipFree(tr);
-            a.sk_trace = nullptr;
-            unsigned long long t0 = ~0ull;
-            for (int p = 0; p < G; ++p) t0 = std::min(t0, t[p * 8]);
-            for (int p = 0; p < G; p += (p < 16 ? 1 : 16)) {
-                printf("sk wg %3d:", p);
-                for (int i = 0; i < 8; ++i) printf(" %7.2f", t[p * 8 + i] ? (t[p * 8 + i] - t0) * 0.01 : -1.0);
-                printf("  (us: start, job ends 1-5, late wait start/end)\n");
-            }
-        }
-    }
     hipFree(A);
     hipFree(W);
     hipFree(Cb);

@@ -172,13 +172,6 @@ struct GemmArgs {
     // compute units of the device the GEMM runs on: the persistent kernels' grid size
     // (0 = assume 256, MI355X)
     int ncu;
-    // stream-K GEMM (gemm_pp.hip, variant 65): fp32 partial slots [grid][256 KB], flags
-    // [grid + 1][8] (the last row: error word), and this launch's epoch (flags equal to it are
-    // this launch's; the caller increments it per launch on a given workspace)
-    void* sk_part;
-    unsigned* sk_flag;
-    unsigned sk_epoch;
-    unsigned long long* sk_trace;  // diagnostic (bench entry only): per-workgroup s_memrealtime stamps
     // 16-row blocked layout (blk16_off) of the 16-bit A operand / C output: c_fc -> c_proj's u.
     // Pipelined (gemm_pipe_kernel) and persistent ping-pong (62 / 63) kernels only; the others
     // refuse it. Rows are padded to a multiple of 16 in the buffer.

@@ -428,9 +428,6 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         unsigned char* sA = smem + buf * STAGE;
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = kbase + (size_t)kt * 128;
-#if CLIPVIT_ABLATE == 1  // diagnostic build only (tools/ablate.sh): no operand fill
-        return;
-#endif
         if constexpr (BUFL) {
             int aofs = a.blk_a ? kt * 2048 : (int)kofs;  // (blk_a: no split-K, launch_pipe)
             if constexpr (PSEP) {  // channel kt / KPC, first pixel row (kt % KPC) * (64 / P)
@@ -540,9 +537,6 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     };
     static_assert(NMF >= NFR, "need at least one MFMA per fragment read");
     auto mfmas = [&](const vec8 (&af)[FM], const vec8 (&wf)[FN]) {
-#if CLIPVIT_ABLATE == 2  // diagnostic build only (tools/ablate.sh): no MFMAs (fragment reads are dead too)
-        return;
-#endif
 #pragma unroll
         for (int fn = 0; fn < FN; ++fn)
 #pragma unroll
@@ -852,12 +846,12 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 only
-        if (variant < 8 || variant == 65 || a.ksplit > 1) return -1;
+    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 only
+        if (variant < 8 || a.ksplit > 1) return -1;
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
-    if (variant >= 62 && variant <= 65) return launch_gemm_pp(s, dtype, epi, a, variant);
+    if (variant == 62 || variant == 63 || variant == 72) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);

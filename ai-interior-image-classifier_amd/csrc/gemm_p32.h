@@ -1,0 +1,322 @@
+// Persistent 256x256 MFMA GEMM with 32-deep k-steps and a four-stage LDS ring (variant 72;
+// round 5). Included by gemm_pp.hip (the library) and tools/probes/gemm_probe.hip (timing).
+//
+//   C[M, N] = A[M, K] @ W[N, K]^T + bias   (16-bit C; QuickGELU for c_fc)
+//
+// What it changes against gemm_ppp_kernel (variant 62), from the r05 timeline probe
+// (profiles/r05_gemm_timeline.md): there, a barrier interval of the k-loop took ~490 cycles for
+// the 256 cycles of MFMA work in it, and the two wave groups' epilogues ran one after the other
+// with no MFMA beside them (~13k of a tile's ~61k cycles). Here:
+//  * a k-step is 32 deep and one wave's segment is 32 MFMAs (all 8 x 4 accumulator fragments of
+//    its 128 x 64 tile, one k-half), so one barrier interval carries 512 MFMA cycles against
+//    12 fragment reads + 4 LDS-DMA pieces of the partner wave (the segment micro-probe:
+//    0.95 of the MFMA rate at that ratio);
+//  * four 32 KB stages: the k-step t + 3 is staged while t is computed, so every LDS-DMA piece
+//    has 4.5-5.5 barrier intervals (~2.5k cycles) to land, against 2-3 in variant 62;
+//  * the code of each wave group is a separate compile-time path (group 0 stages A, group 1
+//    stages W), and the tile-boundary crossing of the k-step stream is unrolled: the k-loop has
+//    no run-time branches; a missing next tile is a zero-length buffer resource (its pieces
+//    read as zeros into a stage nobody reads);
+//  * the bias is the accumulators' initial value (the tile's first MFMAs take it as C), so the
+//    epilogue is QuickGELU (c_fc) + conversion + stores, run in the wave's first read segment
+//    of the next tile, after that segment's fragment reads and staging issue; the stores are
+//    younger than the staged pieces the next waits count, which allow for them.
+//
+// Schedule. Slot = barrier interval. Group g's read segment of k-step t is slot 2t + g, its MFMA
+// segment slot 2t + g + 1 (group 1 runs one barrier behind). Stage s = t & 3 is read in slots 2t
+// and 2t + 1; group 1 retires its reads (lgkmcnt(0)) before the barrier ending slot 2t + 1, so
+// the stage may be refilled from slot 2t + 2: the read segment of step t + 1 stages step t + 4
+// (= issue j + 3 in the segment of step j). Every wave waits for ITS pieces of step t + 1 by a
+// counted vmcnt before the barrier ending slot 2t + 1 (group 0 after its MFMAs, group 1 after its
+// issue), so step t + 1 is complete and visible for both groups' reads.
+//
+// LDS image of a stage: A rows [256][64 B] then W rows [256][64 B]; 16-B chunk c of row r at
+// chunk c ^ ((r >> 2) & 2), which makes the MFMA fragment reads (16 rows x one chunk per
+// quarter-wave) conflict-free on ds_read_b128's lane groups; the LDS-DMA writes lane-linearly,
+// so the swizzle is in the per-lane global source offset. Blocked A (blk16_off, c_proj's u): a
+// 32-deep k-step of a 16-row block is one contiguous 1 KB run, staged verbatim (chunk-major:
+// chunk c, row r at c * 256 + r * 16, also conflict-free).
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+
+namespace clipvit {
+
+template <typename T, int EPI, bool BLKA, int GRP>
+__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc) {
+    typedef typename T::vec8 vec8;
+    constexpr int BM = 256, BN = 256;
+    constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 KB + 16 KB
+    constexpr bool GELU = EPI == EPI_GELU;
+    constexpr bool OWN_BLK = GRP == 0 && BLKA;  // this group's staged operand is the blocked A
+    const float* const colv = (const float*)(smem + 4 * STAGE);
+    const int nM = (a.M + BM - 1) / BM, nN = a.N / BN;
+    const int G = gridDim.x;
+    const size_t ldb = (size_t)a.K * 2;
+    const int nk = a.K >> 5;  // 32-deep k-steps per tile, a multiple of 4
+
+    auto tile = [&](int i, int& m0, int& n0) {
+        const int L = blockIdx.x + i * G;
+        if (L >= ntiles) return false;
+        int mt, nt;
+        tile_of_block(L, nM, nN, a.xcd_n, mt, nt);
+        m0 = mt * BM;
+        n0 = nt * BN;
+        return true;
+    };
+    // this group's operand panel of a tile (A rows for group 0, W rows for group 1)
+    const unsigned char* const src = (const unsigned char*)(GRP == 0 ? a.A : a.W);
+    const int rows = GRP == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;
+    auto rsrc_of = [&](int m0, int n0) {
+        const int r0 = GRP == 0 ? m0 : n0;
+        const size_t bytes = (size_t)(rows - r0) * ldb;
+        return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
+    };
+    const i32x4_t rs_none = buf_rsrc(src, 0u);  // no next tile: reads return zeros
+    // piece i of this wave = 16 rows 16 p .. 16 p + 15 of the panel, p = 4 wc + i
+    unsigned voff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = 4 * wc + i;
+        if constexpr (OWN_BLK) {
+            voff[i] = (unsigned)((size_t)p * 16 * ldb + lane * 16);
+        } else {
+            const int r = lane >> 2, c = (lane & 3) ^ ((lane >> 4) & 2);
+            voff[i] = (unsigned)((16 * p + r) * ldb + c * 16);
+        }
+    }
+    const int opbase = GRP == 0 ? 0 : A_ST;
+    auto koff = [&](int kk) { return OWN_BLK ? (kk >> 1) * 2048 + (kk & 1) * 1024 : kk * 64; };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    auto stage_pieces = [&](const i32x4_t& r, int kk, int st) {
+        unsigned char* dst = smem + st * STAGE + opbase + 4 * wc * 1024;
+        const int so = koff(kk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) blds16(r, voff[i], so, dst + i * 1024);
+    };
+
+    int m0, n0, mn = 0, nn = 0;
+    tile(0, m0, n0);
+    bool has_next = tile(1, mn, nn);
+    i32x4_t rs_c = rsrc_of(m0, n0), rs_n = has_next ? rsrc_of(mn, nn) : rs_none;
+
+    // fragment addresses: lane (row lrow of a 16-row fragment, k-chunk lg)
+    const int lrow = lane & 15, lg = lane >> 4;
+    const int swz = ((lg ^ ((lrow >> 2) & 2)) << 4);
+    const int aoff = BLKA ? (GRP * 128 / 16) * 1024 + lg * 256 + lrow * 16 : (GRP * 128 + lrow) * 64 + swz;
+    constexpr int AFSTEP = BLKA ? 1024 : 1024;  // 16 rows x 64 B either way
+    const int woff = A_ST + (wc * 64 + lrow) * 64 + swz;
+    vec8 af[8], wf[4];
+    f32x4 acc[4][8], bv[4];
+
+    // fragment reads by inline asm off two base registers per operand (stages 0 / 1, and 2 / 3
+    // 64 KB up) with the stage and fragment offsets as immediates below 40 KB. Plain C++ reads
+    // made hipcc keep one address register per read (ds_read's offset field is 16 bits and the
+    // four stages span 128 KB) and spill. The reads are not visible to hipcc's waitcnt pass: every
+    // MFMA segment starts with an explicit lgkmcnt(0) (and a sched_barrier, so nothing that uses
+    // a fragment moves above it), and group 1's read segment ends with one.
+    unsigned a_lo = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + aoff);
+    unsigned w_lo = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + woff);
+    unsigned a_hi, w_hi;
+    asm volatile("v_add_u32 %0, 0x10000, %2\n\tv_add_u32 %1, 0x10000, %3"
+                 : "=v"(a_hi), "=v"(w_hi)
+                 : "v"(a_lo), "v"(w_lo));
+    auto rd = [&](vec8& d, unsigned base, auto imm) {
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
+    };
+    auto reads = [&](auto stc) {
+        constexpr int ST = decltype(stc)::value, SO = (ST & 1) * STAGE;
+        const unsigned ba = ST >= 2 ? a_hi : a_lo, bw = ST >= 2 ? w_hi : w_lo;
+        rd(wf[0], bw, std::integral_constant<int, SO>{});
+        rd(wf[1], bw, std::integral_constant<int, SO + 1024>{});
+        rd(wf[2], bw, std::integral_constant<int, SO + 2048>{});
+        rd(wf[3], bw, std::integral_constant<int, SO + 3072>{});
+        rd(af[0], ba, std::integral_constant<int, SO>{});
+        rd(af[1], ba, std::integral_constant<int, SO + 1 * AFSTEP>{});
+        rd(af[2], ba, std::integral_constant<int, SO + 2 * AFSTEP>{});
+        rd(af[3], ba, std::integral_constant<int, SO + 3 * AFSTEP>{});
+        rd(af[4], ba, std::integral_constant<int, SO + 4 * AFSTEP>{});
+        rd(af[5], ba, std::integral_constant<int, SO + 5 * AFSTEP>{});
+        rd(af[6], ba, std::integral_constant<int, SO + 6 * AFSTEP>{});
+        rd(af[7], ba, std::integral_constant<int, SO + 7 * AFSTEP>{});
+    };
+    auto mfmas = [&](auto first) {
+        constexpr bool FIRST = decltype(first)::value;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm)
+#pragma unroll
+            for (int fn = 0; fn < 4; ++fn) acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // the tile's bias vector slice (16 features per lane) from LDS: inline asm with its own wait
+    // (a plain LDS read makes hipcc drain vmcnt(0): it cannot tell colv from the DMA stages)
+    auto load_bias = [&](int nb) {
+        const unsigned ba = (unsigned)(size_t)(LDS_AS const float*)(colv + nb + wc * 64 + 16 * lg);
+        asm volatile(
+            "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:16\n\tds_read_b128 %2, %4 offset:32\n\t"
+            "ds_read_b128 %3, %4 offset:48\n\ts_waitcnt lgkmcnt(0)"
+            : "=&v"(bv[0]), "=&v"(bv[1]), "=&v"(bv[2]), "=&v"(bv[3])
+            : "v"(ba)
+            : "memory");
+    };
+    unsigned char* const Cb = (unsigned char*)a.C;
+    auto epilogue = [&](int pm0, int pn0) {
+        // lane-derived addresses recomputed here from an opaque copy of the lane id: hipcc
+        // otherwise hoists the per-row offsets of all 16 stores out of the tile loop and spills
+        int le;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
+        const int n = pn0 + wc * 64 + 16 * (le >> 4);
+#pragma unroll
+        for (int fm = 0; fm < 8; ++fm) {
+            const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
+            float v[16];
+#pragma unroll
+            for (int f = 0; f < 4; ++f)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+            if constexpr (GELU) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
+                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.4554669595930156f * v[q]));
+            }
+            if (m < a.M) {
+                const size_t off = a.blk_c ? blk16_off(m, n, a.ldc) : ((size_t)m * a.ldc + n) * 2;
+                const size_t off2 = a.blk_c ? off + 256 : off + 16;
+                const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+                const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
+                                  pack2<T>(v[14], v[15])};
+                *(u32x4*)(Cb + off) = w0;
+                *(u32x4*)(Cb + off2) = w1;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
+        }
+    };
+
+    // vmcnt allowances: 8 = the two younger issue groups of 4 pieces; 24 when the previous
+    // tile's 16 epilogue stores are also younger than the awaited pieces. On a workgroup's first
+    // tile there is no previous tile: 16 stores through a zero-length buffer resource (dropped by
+    // the range check) take the epilogue's place, so the counts and the code are the same.
+    const i32x4_t rs_drop = buf_rsrc(a.C, 0u);
+    auto null_stores = [&]() {  // inline asm: hipcc would merge 16 identical stores into one
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        asm volatile(
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0"
+            :
+            : "v"(z), "s"(rs_drop)
+            : "memory");
+    };
+    //
+    // one k-step (compile-time position): ST / STI = stage read / staged; NXT = the staged step
+    // belongs to the next tile (kk = step within that tile); FIRST = the tile's first step (bias
+    // as the accumulators' initial value); EP = it carries the previous tile's epilogue; W24 =
+    // wait allowance 24 instead of 8
+    auto kstep = [&](int kk_issue, auto nxt, auto stc, auto stic, auto first, auto ep, auto w24, bool have_prev,
+                     int pm0, int pn0) {
+        constexpr bool EP = decltype(ep)::value;
+        constexpr bool W24 = decltype(w24)::value;
+        // ---- read segment: staging issue first (it does not wait for anything), then group 1's
+        // counted wait, the previous tile's epilogue (its stores younger than every piece the
+        // next waits count), the tile's bias slice, the fragment reads ----
+        stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value);
+        if constexpr (GRP == 1) {  // pieces of step t + 1 (issued two read segments ago) landed
+            if (W24) vm_wait<24>(); else vm_wait<8>();
+        }
+        if constexpr (EP) {
+            if (have_prev) epilogue(pm0, pn0);
+            else null_stores();
+        }
+        if constexpr (decltype(first)::value) load_bias(n0);
+        reads(stc);
+        if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
+        bar();
+        // ---- MFMA segment ----
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // the fragment reads (inline asm) landed
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(first);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (GRP == 0) {
+            if (W24) vm_wait<24>(); else vm_wait<8>();
+        }
+        bar();
+    };
+    // prologue: steps 0, 1, 2 of the first tile; the bias vector of the whole GEMM -> LDS
+    stage_pieces(rs_c, 0, 0);
+    stage_pieces(rs_c, 1, 1);
+    stage_pieces(rs_c, 2, 2);
+    {
+        float* cv = (float*)(smem + 4 * STAGE);
+        for (int i = (GRP * 256 + wc * 64 + lane); i < a.N; i += 512) cv[i] = a.bias ? a.bias[i] : 0.f;
+    }
+    vm_wait<0>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    if constexpr (GRP == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    using S3 = std::integral_constant<int, 3>;
+    using W0 = std::integral_constant<bool, GRP == 0>;  // group 0 waits after its epilogue's stores
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) acc[f][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int pm0 = 0, pn0 = 0;
+    for (int i = 1;; ++i) {
+        const bool have_prev = i > 1;
+        // first group of four steps (0..3): step 0 carries the previous tile's epilogue
+        kstep(3, F_{}, S0{}, S3{}, T_{}, T_{}, W0{}, have_prev, pm0, pn0);
+        kstep(4, F_{}, S1{}, S0{}, F_{}, F_{}, T_{}, false, 0, 0);
+        kstep(5, F_{}, S2{}, S1{}, F_{}, F_{}, T_{}, false, 0, 0);
+        kstep(6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        for (int kt = 4; kt < nk - 4; kt += 4) {
+            kstep(kt + 3, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 4, F_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 5, F_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        }
+        // last group: steps nk - 4 .. nk - 1 stage nk - 1, then the next tile's steps 0, 1, 2
+        // (nk >= 8: the launcher refuses K < 256)
+        kstep(nk - 1, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(0, T_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(1, T_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(2, T_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        pm0 = m0;
+        pn0 = n0;
+        if (!has_next) break;
+        m0 = mn;
+        n0 = nn;
+        rs_c = rs_n;
+        has_next = tile(i + 1, mn, nn);
+        rs_n = has_next ? rsrc_of(mn, nn) : rs_none;
+    }
+    epilogue(pm0, pn0);
+    if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+    vm_wait<0>();
+}
+
+template <typename T, int EPI, bool BLKA>
+__global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave < 4) p32_body<T, EPI, BLKA, 0>(a, ntiles, smem, lane, wave);
+    else p32_body<T, EPI, BLKA, 1>(a, ntiles, smem, lane, wave - 4);
+}
+
+}  // namespace clipvit

@@ -211,16 +211,22 @@ DEFAULT_PROFILE = ROOT / "profiles" / "r04b_fc_traffic.json"  # committed by too
 
 def load_traffic(path: str | None):
     """The c_fc figures of a rocprofv3 profile of this same command (tools/profile_round.sh: kernel
-    trace + separate PMC passes; it passes --traffic-json to its own bench run). Without the flag,
-    the committed profile of the current build (DEFAULT_PROFILE), labelled as such. Returns
-    (dict or None, source)."""
-    p = Path(path) if path else DEFAULT_PROFILE
+    trace + separate PMC passes; it passes --traffic-json to its own bench run). Only a profile
+    named by --traffic-json fills the line's `traffic` / `rocprof`; without the flag those stay
+    null and the committed profile (DEFAULT_PROFILE) is reported apart, as `reference_profile`
+    (numbers of another build must not sit beside this run's). Returns
+    (this run's dict or None, its source, the reference dict or None)."""
+    if path:
+        try:
+            d = json.loads(Path(path).read_text())
+        except (OSError, ValueError):
+            return None, None, None
+        return d, d.get("source", str(path)), None
     try:
-        d = json.loads(p.read_text())
+        ref = json.loads(DEFAULT_PROFILE.read_text())
     except (OSError, ValueError):
-        return None, None
-    src = d.get("source", str(p))
-    return d, (src if path else f"committed profile ({src}), not this run")
+        ref = None
+    return None, None, ref
 
 
 def reconcile(fam: dict, step_ms: float):
@@ -347,8 +353,14 @@ def main():
     gflop_img = cfg.gflop_per_image() - pruned
     model_tflops = value / world * gflop_img / 1e3
 
-    prof, traffic_src = load_traffic(a.traffic_json)
+    prof, traffic_src, ref_prof = load_traffic(a.traffic_json)
     traffic = prof.get("fc_gemm_bytes_per_launch") if prof else None
+    reference_profile = None
+    if ref_prof:  # committed profile of an earlier build: context only, never this run's figures
+        reference_profile = {"file": str(DEFAULT_PROFILE.relative_to(ROOT)), "source": ref_prof.get("source"),
+                             "fc_gemm_avg_us": ref_prof.get("fc_gemm_avg_us"),
+                             "fc_gemm_bytes_per_launch": ref_prof.get("fc_gemm_bytes_per_launch"),
+                             "note": "committed profile of an earlier build, not this run"}
     rocprof = None
     if prof and prof.get("fc_gemm_avg_us"):  # the rocprof figure beside this line's event timing
         rocprof = {"avg_launch_us": round(prof["fc_gemm_avg_us"], 2),
@@ -386,6 +398,7 @@ def main():
                      "rocprof": rocprof if a.dtype == "fp16" and a.batch == 256 and cfg.name == "ViT-B/32" else None,
                      "traffic": traffic if a.dtype == "fp16" and a.batch == 256 and cfg.name == "ViT-B/32" else None,
                      "traffic_source": traffic_src,
+                     "reference_profile": reference_profile,
                      "flop_per_launch": mlp_flop, "images_per_launch": lane_b, "avg_launch_ms": round(fc_ms, 5),
                      "mlp_pair_frac": round(mlp_flop / (mlp_ms * 1e-3) / 1e12 / peak, 4),
                      "model_mfma_frac": round(model_tflops / peak, 4),

@@ -30,14 +30,13 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # 34xx / 35xx = column-group-major 1-D remap with 2 / 3 N-groups (tile_of_block).
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 62 the persistent 256x256 ping-pong tile
-# (gemm_pp.hip; 63 the same with non-temporal stores; 65 stream-K: every CU an equal share
-# of the k-tile iterations, split tiles combined through fp32 partial slots; whole tiles where a
-# share would be shorter than one tile's k-tiles);
+# (gemm_pp.hip; 63 the same with non-temporal stores; 72 the 32-deep-k-step persistent tile of
+# gemm_p32.h);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 22, 62, 63, 65, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3465, 3480]
+VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472, 3480]
 N128 = (1, 2, 22, 81, 82)
-N256 = (3, 8, 62, 63, 65, 80, 98)
-STAGED = (62, 63, 65, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 62, 63, 72, 80, 98)
+STAGED = (62, 63, 72, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -52,8 +51,10 @@ def _skip(variant, N, K):
     v = variant % 100
     if (v in N128 and N % 128) or (v in N256 and N % 256):
         return "tile does not divide N"
-    if v in (62, 63, 65) and K % 128:
+    if v in (62, 63) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
+    if v == 72 and (K % 128 or K < 256):
+        return "32-deep-k-step tile: K a multiple of 128, >= 256"
     return None
 
 
@@ -75,36 +76,11 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("epi", [10, 11])
-@pytest.mark.parametrize("variant", [65, 3465])
-@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768),    # B/32 c_fc at bs 256: 28-29 k-tiles per CU
-                                   (12763, 3072, 768),    # ragged last row tile
-                                   (9000, 2304, 1024),    # 20-21 of 16 k-tiles, ragged
-                                   (8000, 2304, 1536),    # nk 24: 27 per CU, shares just above a tile
-                                   (4096, 4096, 1024)])   # one whole tile per CU (no split)
-def test_gemm_stream_k(gpu, dtype, epi, variant, M, N, K):
-    """Stream-K (variant 65): tiles split between two CUs are combined through the fp32 partial
-    slots (EARLY suffix stored with sc1 write-through stores, LATE prefix accumulated on top of
-    the loaded partial). Every output element against the fp32 reference (16-bit output), and two
-    launches bit-identical (the partition, hence the arithmetic, is fixed by the shape)."""
-    g = torch.Generator(device=gpu).manual_seed(M + N + K + epi)
-    A = torch.randn(M, K, device=gpu, generator=g).to(dtype)
-    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
-    bias = torch.randn(N, device=gpu, generator=g)
-    C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
-    C2 = E.gemm_test(A, W, bias, epi=epi, variant=variant)
-    ref = _ref_gemm(A, W, bias, epi - 10)
-    err = (C - ref).abs().max().item() / ref.abs().max().item()
-    assert err < (8e-3 if dtype == torch.bfloat16 else 2e-3), err
-    assert torch.equal(C, C2)
-
-
 @pytest.mark.parametrize("variant", STAGED + (8, 22))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous
-    (80-82, 98) and direct from the accumulators (8, 22, 62, 63, 65)."""
+    (80-82, 98) and direct from the accumulators (8, 22, 62, 63, 72)."""
     dtype = torch.float16
     M, N, K = 1000, 2304, 768
     if N % (256 if variant in N256 else 128):

@@ -1,6 +1,6 @@
 #!/bin/bash
-# r04 second session: bench lines of the other BASELINE configs on the final build (config 4
-# L/14@336 bs 128 fp16, B/16 bs 256 fp16, config 2 in bf16 at bs 256) and the default line
+# Bench lines of the other BASELINE configs (config 4 L/14@336 bs 128 fp16, B/16 bs 256 fp16,
+# config 2 in bf16 at bs 256) and the default line
 set -o pipefail
 mkdir -p gpurun_out/cfg
 timeout -k 10 300 python -u bench.py --model ViT-L/14@336px --batch 128 --lora-rank 16 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/cfg/cfg4.json 2> gpurun_out/cfg/cfg4.err || { echo "cfg4 failed"; tail -5 gpurun_out/cfg/cfg4.err; exit 1; }

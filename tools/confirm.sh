@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04 closing check at HEAD: full GPU test suite, the default bench line and the config-5 pair
+# Closing check at HEAD: full GPU test suite, the default bench line and the config-5 pair
 # (MX-fp8 and bf16 at bs 512). Every GPU step under its own time limit; the first failure ends
 # the call.
 set -o pipefail
