@@ -66,11 +66,11 @@ def gpu_worker(rank, world, port, B, q):
         a, b = dp.shard_bounds(B, world, rank)
         logits, res = dp.ShardedClassifier(eng).classify_global(full[a:b].to(dev), B)
         torch.cuda.synchronize()
-        ok = True
+        ok = tuple(logits.shape) == (B, 437)
         if rank == 0:
             one = eng.classify(full.to(dev))
             torch.cuda.synchronize()
-            ok = torch.equal(logits.cpu(), one.logits.cpu()) and \
+            ok = ok and torch.equal(logits.cpu(), one.logits.cpu()) and \
                 torch.equal(res.top_idx.cpu(), one.top_idx[a:b].cpu())
         eng.close()
         q.put((rank, bool(ok)))
