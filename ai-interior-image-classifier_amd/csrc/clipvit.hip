@@ -61,6 +61,8 @@ struct DeviceGuard {
 
 struct LayerW {
     void *wqkv = nullptr, *wout = nullptr, *wfc = nullptr, *wproj = nullptr;
+    // QKV / c_fc weights again in the 16-row blocked layout (GemmArgs.blk_w), with w_blocked
+    void *wqkv_b = nullptr, *wfc_b = nullptr;
     const float *bqkv, *bout, *bfc, *bproj, *ln1g, *ln1b, *ln2g, *ln2b;
     // LayerNorm fold (lnfold): ln_1 into QKV, ln_2 into c_fc: s_n = sum_k W'_nk, b' = b + W beta
     float *s_qkv = nullptr, *bf_qkv = nullptr, *s_fc = nullptr, *bf_fc = nullptr;
@@ -251,6 +253,7 @@ struct clipvit_handle {
     // accumulator-layout stores become 256-B runs per quarter-wave instead of 16 scattered
     // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
     bool u_blk = true;
+    bool w_blk = false;  // tuning w_blocked: QKV / c_fc weights also in the 16-row blocked layout
 };
 
 static std::string L(int i, const char* leaf) {
@@ -409,7 +412,7 @@ struct Fold {
 
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
                 const float* bias, void* C, int M, int N, int K, int ldc, int role, const Fold& fo = Fold(),
-                Lane* lane = nullptr) {
+                Lane* lane = nullptr, const void* Wb = nullptr) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
@@ -424,6 +427,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.blk_c = ublk && role == R_FC;
     a.blk_a = ublk && role == R_PROJ;
     int variant = h->var[role];
+    // the blocked copy of W (w_blocked) for the launches whose tile reads it
+    auto wsel = [&](GemmArgs& g, int v) {
+        const bool blk = Wb && h->w_blk && v >= 8 && v != 62 && v != 63 && g.ksplit <= 1;
+        g.W = blk ? Wb : W;
+        g.blk_w = blk;
+    };
     // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
     // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
     // lower LDS fill per FLOP wins — measured: config 4 1,918 -> 2,072 img/s; B/16 c_fc (2,364
@@ -460,8 +469,10 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             if (c.st_in) c.st_in += (size_t)m1 * c.np;
             c.M = M - (int)m1;
             c.xcd_n = h->xcd[role];  // tail: the role's partition (main: 1-D, whole rounds per XCD)
-            if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 &&
-                launch_gemm(s, h->dt, epi, c, h->split_tail ? h->split_tail : variant) == 0)
+            const int tv = h->split_tail ? h->split_tail : variant;
+            wsel(b, h->split_main);
+            wsel(c, tv);
+            if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 && launch_gemm(s, h->dt, epi, c, tv) == 0)
                 return 0;
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
@@ -480,7 +491,10 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
         }
     }
     // a tuned variant that does not tile this shape falls back to the shape-based choice
-    if (launch_gemm(s, h->dt, epi, a, variant) != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
+    wsel(a, variant);
+    int rc = launch_gemm(s, h->dt, epi, a, variant);
+    wsel(a, 0);
+    if (rc != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
                 " K=" + std::to_string(K);
         return CLIPVIT_E_INVALID;
@@ -662,7 +676,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         // q: the attention roles (QKV, out_proj) in MX-fp8; qm: the MLP roles
         const bool q = h->q8_attn(i), qm = h->q8_mlp(i), last = i + 1 == h->cfg.layers;
         rc = q ? gemm8(s, h, EPI_STORE, q8, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV)
-               : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w);
+               : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b);
         if (rc) return rc;
         if (prof) prof->mark(s, F_QKV);
         if (!q || !h->attn_q8 || launch_attention_q8(s, h->dt, w->qkv, q8, q8s, B, N, h->cfg.heads) != 0) {
@@ -690,7 +704,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         // (the fp32 residual c_proj runs on the other MX tiles: row-major u8)
         const bool ublk = h->u_blk && p16 && h->var8[R_FC] == 3 && h->var8[R_PROJ] == 3;
         rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC, ublk)
-               : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w);
+               : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b);
         if (rc) return rc;
         if (prof) prof->mark(s, F_FC);
         const int ep = p16 ? EPI_STORE : EPI_RESID;
@@ -831,7 +845,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
         const bool last = i + 1 == nl;
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w)))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
@@ -853,7 +867,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
         }
         if (prof) prof->mark(s, F_LN);
-        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w)))
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b)))
             return rc;
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
@@ -963,6 +977,11 @@ static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name
         }
     }
     launch_pack_weight(s, h->dt, w, dst, N, K, Kp);
+    if (layer >= 0) {  // the blocked copy (w_blocked) follows every re-pack (LoRA merges too)
+        const LayerW& ly = h->layers[layer];
+        void* blk = dst == ly.wqkv ? ly.wqkv_b : dst == ly.wfc ? ly.wfc_b : nullptr;
+        if (blk) launch_blk16_relayout(s, dst, blk, N, Kp);
+    }
     return 0;
 }
 
@@ -1076,15 +1095,17 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     bool ok = true;
     if (k == "resid16") ok = flag(h->resid16);
     else if (k == "defer_x") ok = flag(h->defer_x);
-    else if (k == "lnfold") ok = flag(h->lnfold);  // resolved after every key (clipvit_set_tuning) else if (k == "cls_prune") ok = flag(h->cls_prune);
+    else if (k == "lnfold") ok = flag(h->lnfold);  // resolved after every key (clipvit_set_tuning)
+    else if (k == "cls_prune") ok = flag(h->cls_prune);
     else if (k == "round_split") ok = flag(h->round_split);
     else if (k == "attn_q8") ok = flag(h->attn_q8);
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
-    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63)
+    else if (k == "w_blocked") ok = flag(h->w_blk);
+    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63);
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
@@ -1098,6 +1119,13 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         ok = parse_int(v, x);
         if (ok) h->split_min = x <= 0 ? SPLIT_NEVER : x;
     } else if (k == "gemm_xcd") ok = parse_list(v, h->xcd, 5);
+    else if (k == "qkv_variant") {  // 100 * XCD map + tile of the QKV role, shape rules kept (gemm_variants forces all)
+        ok = parse_int(v, x) && x > 0;
+        if (ok) {
+            h->var[R_QKV] = x % 100;
+            h->xcd[R_QKV] = x / 100;
+        }
+    }
     else if (k == "mx8_skip") {  // both masks
         ok = parse_mask(v, h->mx8_skip);
         if (ok) h->mx8_skip_mlp = h->mx8_skip;
@@ -1133,14 +1161,14 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, w_blk;
         int split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->w_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1156,6 +1184,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
+            h->w_blk = before.w_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1218,12 +1247,17 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
+    const bool wblk = h->w_blk && !h->mx8;  // blocked QKV / c_fc weight copies
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         HIPCHK(alloc16(ly.wqkv, 3 * D * D));
         HIPCHK(alloc16(ly.wout, D * D));
         HIPCHK(alloc16(ly.wfc, 4 * D * D));
         HIPCHK(alloc16(ly.wproj, 4 * D * D));
+        if (wblk) {
+            HIPCHK(alloc16(ly.wqkv_b, 3 * D * D));
+            HIPCHK(alloc16(ly.wfc_b, 4 * D * D));
+        }
         ly.bqkv = h->master[L(i, "attn.in_proj_bias")];
         ly.bout = h->master[L(i, "attn.out_proj.bias")];
         ly.bfc = h->master[L(i, "mlp.c_fc.bias")];
@@ -1479,6 +1513,8 @@ int clipvit_destroy(clipvit_handle* h) {
         hipFree(ly.wqkv);
         hipFree(ly.wout);
         hipFree(ly.wfc);
+        hipFree(ly.wqkv_b);
+        hipFree(ly.wfc_b);
         hipFree(ly.wproj);
     }
     hipFree(h->scratch);
@@ -1515,10 +1551,20 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     void* Wp = nullptr;
     HIPCHK(hipMallocAsync(&Wp, (size_t)N * K * 2, s));
     launch_pack_weight(s, dtype, (const float*)W_dev, Wp, N, K, K);
+    const bool wblk = variant >= 10000;  // + 10000: W in the blocked layout (GemmArgs.blk_w)
+    variant %= 10000;
+    if (wblk) {  // relayout in place through a copy
+        void* Wr = nullptr;
+        HIPCHK(hipMallocAsync(&Wr, (size_t)N * K * 2, s));
+        HIPCHK(hipMemcpyAsync(Wr, Wp, (size_t)N * K * 2, hipMemcpyDeviceToDevice, s));
+        launch_blk16_relayout(s, Wr, Wp, N, K);
+        HIPCHK(hipFreeAsync(Wr, s));
+    }
     GemmArgs a{};
     a.A = A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.ncu = current_ncu();
+    a.blk_w = wblk;
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
@@ -1624,6 +1670,8 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.A = A; a.W = W; a.bias = bias; a.C = Cb;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.patch_g2 = 49; a.patch_ntok = 50;
+    a.blk_w = variant >= 10000;  // (random operands: the layout only changes the access pattern)
+    variant %= 10000;
     a.xcd_n = variant / 100;
     variant %= 100;
     a.ncu = current_ncu();

@@ -181,6 +181,10 @@ struct GemmArgs {
     // consecutive rows are one contiguous run (0 = row-major [rows][K / 32] bytes). sc_rows = the
     // padded row count of the whole matrix (a row-split launch passes its parent's)
     int sc_rows;
+    // W in the 16-row blocked layout (blk16_off over its packed rows, launch_blk16_relayout): a
+    // 64-deep k-tile of 16 weight rows is one contiguous 2 KB run. Pipelined tiles (8..98, not the
+    // patch GEMM) and the 32-deep-k-step persistent tile (72) only.
+    int blk_w;
 };
 
 // 16-row blocked layout of a 16-bit [rows, ncols] matrix (ncols % 64 == 0): 16 x 64 blocks of
@@ -380,6 +384,7 @@ void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const f
                       const float* b, int rows, int D);
 void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,
                         int Kp);
+void launch_blk16_relayout(hipStream_t s, const void* src, void* dst, int rows, int cols);
 void launch_fill_random16(hipStream_t s, int dtype, void* p, size_t n, unsigned seed);
 void launch_lora_merge(hipStream_t s, float* W, const float* A, const float* Bm, int in_f,
                        int out_f, int rank, float scaling);

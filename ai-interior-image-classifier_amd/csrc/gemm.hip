@@ -395,8 +395,16 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     if constexpr (BUFL) {
         const size_t wbytes = (size_t)(a.N - n0) * ldb;
         rsW = buf_rsrc(Wb + (size_t)n0 * ldb, (unsigned)min(wbytes, (size_t)0xFFFFFFFFu));
+        if (a.blk_w) {  // blocked W (blk16_off over the packed rows): the blk_a form below
 #pragma unroll
-        for (int r = 0; r < LW; ++r) bow[r] = (unsigned)(wsrc[r] - (size_t)n0 * ldb);
+            for (int r = 0; r < LW; ++r) {
+                const int p = r * NT * 16 + tid * 16;
+                bow[r] = (unsigned)((size_t)(p >> 11) * 16 * ldb + (p & 2047));
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < LW; ++r) bow[r] = (unsigned)(wsrc[r] - (size_t)n0 * ldb);
+        }
         if constexpr (PSEP) {
             constexpr int CPR = PIMPL / 8;  // 16-B chunks per pixel row of a patch
             const size_t img = (size_t)3 * a.patch_R * a.patch_Rw * 2;  // bytes per image
@@ -429,7 +437,8 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         unsigned char* sW = sA + A_BYTES;
         const size_t kofs = kbase + (size_t)kt * 128;
         if constexpr (BUFL) {
-            int aofs = a.blk_a ? kt * 2048 : (int)kofs;  // (blk_a: no split-K, launch_pipe)
+            int aofs = a.blk_a ? kt * 2048 : (int)kofs;  // (blk_a / blk_w: no split-K, launch_pipe)
+            const int wofs = a.blk_w ? kt * 2048 : (int)kofs;
             if constexpr (PSEP) {  // channel kt / KPC, first pixel row (kt % KPC) * (64 / P)
                 constexpr int KPC = PIMPL * PIMPL / 64;
                 aofs = ((kt / KPC) * a.patch_R + (kt % KPC) * (64 / PIMPL)) * a.patch_Rw * 2;
@@ -439,7 +448,7 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                 if (r * NT * 16 + wave * 1024 < A_BYTES) blds16(rsA, boa[r], aofs, sA + r * NT * 16 + wave * 1024);
 #pragma unroll
             for (int r = 0; r < LW; ++r)
-                if (r * NT * 16 + wave * 1024 < W_BYTES) blds16(rsW, bow[r], (int)kofs, sW + r * NT * 16 + wave * 1024);
+                if (r * NT * 16 + wave * 1024 < W_BYTES) blds16(rsW, bow[r], wofs, sW + r * NT * 16 + wave * 1024);
             return;
         }
 #pragma unroll
@@ -456,17 +465,18 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
     // A fragment of row lrow, k-chunk (s << 2) | lg: swizzled row-major image, or (blk_a) the
     // chunk-major image of the 16-row blocks (chunk * 256 + row * 16, conflict-free unswizzled)
-    const bool ablk = a.blk_a != 0;
+    const bool ablk = a.blk_a != 0, wblk = BUFL && a.blk_w != 0;
     const int aoff = ablk ? wm * TM * 128 + lrow * 16 : (wm * TM + lrow) * 128;
-    const int woff = A_BYTES + (wn * TN + lrow) * 128;
+    const int woff = A_BYTES + (wblk ? wn * TN * 128 + lrow * 16 : (wn * TN + lrow) * 128);
     auto load_frags = [&](int buf, int s, vec8 (&af)[FM], vec8 (&wf)[FN]) {
         const unsigned char* base = smem + buf * STAGE;
         const int c = (((s << 2) | lg) ^ lsw) << 4;
         const int ca = ablk ? ((s << 2) | lg) << 8 : c;
+        const int cw = wblk ? ((s << 2) | lg) << 8 : c;
 #pragma unroll
         for (int fm = 0; fm < FM; ++fm) af[fm] = *(const vec8*)(base + aoff + fm * 2048 + ca);
 #pragma unroll
-        for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + c);
+        for (int fn = 0; fn < FN; ++fn) wf[fn] = *(const vec8*)(base + woff + fn * 2048 + cw);
     };
 
     f32x4 acc[FN][FM];
@@ -846,11 +856,13 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 only
+    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 / 73 only
         if (variant < 8 || a.ksplit > 1) return -1;
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
+    // blocked W: the pipelined tiles and the 32-deep-k-step persistent tile
+    if (a.blk_w && (variant < 8 || variant == 62 || variant == 63 || a.ksplit > 1)) return -1;
     if (variant == 62 || variant == 63 || variant == 72) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

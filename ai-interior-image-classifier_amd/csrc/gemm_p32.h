@@ -43,13 +43,38 @@
 
 namespace clipvit {
 
-template <typename T, int EPI, bool BLKA, int GRP>
-__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc) {
+// Barrier policy of the kernel: the library's is the plain s_barrier. tools/probes/gemm_probe.hip
+// instantiates the kernel with a policy that also stamps s_memtime around every barrier (the
+// timeline of profiles/r05_gemm_timeline.md); the instruction stream between barriers is the same.
+struct P32Barrier {
+    __device__ __forceinline__ void bar(int /*tile*/, int /*step*/, int /*seg*/) { __builtin_amdgcn_s_barrier(); }
+    __device__ __forceinline__ void mark(int /*tile*/, int /*which*/) {}
+    __device__ __forceinline__ void sub(int /*tile*/, int /*step*/) {}
+    __device__ __forceinline__ void init(unsigned char*, int, int) {}
+    __device__ __forceinline__ void done(const GemmArgs&) {}
+};
+
+__device__ void p32_store16(u32x4 vdata, i32x4_t rsrc, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.raw.buffer.store.v4i32");
+
+// STP: cache policy of the epilogue stores (0 = plain global stores; else the aux bits of a
+// buffer store: 16 = sc1, which writes through without keeping the line in the XCD's L2, 2 = nt)
+// ROT: each tile walks its k-steps from (nt & 3) * nk / 4 on, wrapping (diagnostic: CUs that
+// share an operand panel then request different k-slices at a given time)
+// RES (diagnostic, outputs garbage): 1 = every tile stages the first W panel, 2 = the first A
+// panel, so that operand is an L2 hit after its first fetch
+// ABL (diagnostic, outputs garbage): 7 = no staging after the prologue, 8 = no MFMA, 9 = no
+// fragment reads, 3 = no epilogue stores
+template <typename T, int EPI, bool BLKA, bool BLKW, int STP, int GRP, class HK, bool ROT = false, int RES = 0,
+          bool RD1 = false, int ABL = 0>
+__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
     constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 KB + 16 KB
     constexpr bool GELU = EPI == EPI_GELU;
-    constexpr bool OWN_BLK = GRP == 0 && BLKA;  // this group's staged operand is the blocked A
+    // this group's staged operand is in the 16-row blocked layout (blk16_off): the blocked A
+    // (c_proj's u) or a blocked weight
+    constexpr bool OWN_BLK = (GRP == 0 && BLKA) || (GRP == 1 && BLKW);
     const float* const colv = (const float*)(smem + 4 * STAGE);
     const int nM = (a.M + BM - 1) / BM, nN = a.N / BN;
     const int G = gridDim.x;
@@ -67,9 +92,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     };
     // this group's operand panel of a tile (A rows for group 0, W rows for group 1)
     const unsigned char* const src = (const unsigned char*)(GRP == 0 ? a.A : a.W);
-    const int rows = GRP == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;
+    const int rows = GRP == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;  // (N % 256 == 0)
     auto rsrc_of = [&](int m0, int n0) {
-        const int r0 = GRP == 0 ? m0 : n0;
+        int r0 = GRP == 0 ? m0 : n0;
+        if constexpr (RES == 1) { if (GRP == 1) r0 = 0; }
+        if constexpr (RES == 2) { if (GRP == 0) r0 = 0; }
         const size_t bytes = (size_t)(rows - r0) * ldb;
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
     };
@@ -90,9 +117,15 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     auto koff = [&](int kk) { return OWN_BLK ? (kk >> 1) * 2048 + (kk & 1) * 1024 : kk * 64; };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    auto stage_pieces = [&](const i32x4_t& r, int kk, int st) {
+    int rot_c = 0, rot_n = 0;  // (ROT) k-step rotation of the current / next tile
+    auto stage_pieces = [&](const i32x4_t& r, int kk, int st, int rot) {
         unsigned char* dst = smem + st * STAGE + opbase + 4 * wc * 1024;
+        if constexpr (ROT) {
+            kk += rot;
+            if (kk >= nk) kk -= nk;
+        }
         const int so = koff(kk);
+        if constexpr (ABL == 7) return;
 #pragma unroll
         for (int i = 0; i < 4; ++i) blds16(r, voff[i], so, dst + i * 1024);
     };
@@ -107,7 +140,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     const int swz = ((lg ^ ((lrow >> 2) & 2)) << 4);
     const int aoff = BLKA ? (GRP * 128 / 16) * 1024 + lg * 256 + lrow * 16 : (GRP * 128 + lrow) * 64 + swz;
     constexpr int AFSTEP = BLKA ? 1024 : 1024;  // 16 rows x 64 B either way
-    const int woff = A_ST + (wc * 64 + lrow) * 64 + swz;
+    const int woff = BLKW ? A_ST + (wc * 4) * 1024 + lg * 256 + lrow * 16 : A_ST + (wc * 64 + lrow) * 64 + swz;
     vec8 af[8], wf[4];
     f32x4 acc[4][8], bv[4];
 
@@ -128,6 +161,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     };
     auto reads = [&](auto stc) {
         constexpr int ST = decltype(stc)::value, SO = (ST & 1) * STAGE;
+        if constexpr (ABL == 9) return;
         const unsigned ba = ST >= 2 ? a_hi : a_lo, bw = ST >= 2 ? w_hi : w_lo;
         rd(wf[0], bw, std::integral_constant<int, SO>{});
         rd(wf[1], bw, std::integral_constant<int, SO + 1024>{});
@@ -148,12 +182,16 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm)
 #pragma unroll
-            for (int fn = 0; fn < 4; ++fn) acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+            for (int fn = 0; fn < 4; ++fn) {
+                if constexpr (ABL == 8) asm volatile("" ::"v"(wf[fn]), "v"(af[fm]));
+                else acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+            }
         __builtin_amdgcn_s_setprio(0);
     };
-    auto bar = [&]() {
+    int ti = 0;  // tiles done by this workgroup (barrier policy only)
+    auto bar = [&](int step, int seg) {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        hk.bar(ti, step, seg);
         __builtin_amdgcn_sched_barrier(0);
     };
     // the tile's bias vector slice (16 features per lane) from LDS: inline asm with its own wait
@@ -168,6 +206,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             : "memory");
     };
     unsigned char* const Cb = (unsigned char*)a.C;
+    const i32x4_t rs_out = buf_rsrc(a.C, 0xFFFFFFFFu);  // (STP != 0) C < 4 GB
     auto epilogue = [&](int pm0, int pn0) {
         // lane-derived addresses recomputed here from an opaque copy of the lane id: hipcc
         // otherwise hoists the per-row offsets of all 16 stores out of the tile loop and spills
@@ -187,14 +226,37 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                 for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
                     v[q] *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.4554669595930156f * v[q]));
             }
-            if (m < a.M) {
-                const size_t off = a.blk_c ? blk16_off(m, n, a.ldc) : ((size_t)m * a.ldc + n) * 2;
-                const size_t off2 = a.blk_c ? off + 256 : off + 16;
-                const u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
-                const u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]),
-                                  pack2<T>(v[14], v[15])};
-                *(u32x4*)(Cb + off) = w0;
-                *(u32x4*)(Cb + off2) = w1;
+            u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
+            u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
+            size_t off, off2;
+            if (a.blk_c) {  // blocked C: each quarter-wave already writes 256 contiguous bytes
+                off = blk16_off(m, n, a.ldc);
+                off2 = off + 256;
+            } else {
+                // row-major C: lane group g holds features [16g, 16g + 16) of the wave's 64-column
+                // slice, so plain stores leave 4 scattered 16-B pieces per row and instruction.
+                // One permlane32 swap per dword (groups 2-3 of w0 <-> groups 0-1 of w1) gives
+                // w0 = {P0, P1, Q0, Q1} = features [0, 32) and w1 = {P2, P3, Q2, Q3} = [32, 64)
+                // (P = first, Q = second half of a group's 16 features): 64 contiguous bytes per
+                // row and instruction. Both lanes of a swap pair own the same row (same m).
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(w0[d], w1[d], false, false);
+                    w0[d] = r[0];
+                    w1[d] = r[1];
+                }
+                const int g = le >> 4;
+                off = ((size_t)m * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
+                off2 = off + 64;
+            }
+            if (m < a.M && (ABL != 3 || a.ldc < 0)) {
+                if constexpr (STP == 0) {
+                    *(u32x4*)(Cb + off) = w0;
+                    *(u32x4*)(Cb + off2) = w1;
+                } else {
+                    p32_store16(w0, rs_out, (int)off, 0, STP);
+                    p32_store16(w1, rs_out, (int)off2, 0, STP);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
         }
@@ -225,25 +287,31 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     // belongs to the next tile (kk = step within that tile); FIRST = the tile's first step (bias
     // as the accumulators' initial value); EP = it carries the previous tile's epilogue; W24 =
     // wait allowance 24 instead of 8
-    auto kstep = [&](int kk_issue, auto nxt, auto stc, auto stic, auto first, auto ep, auto w24, bool have_prev,
-                     int pm0, int pn0) {
+    auto kstep = [&](int step, int kk_issue, auto nxt, auto stc, auto stic, auto first, auto ep, auto w24,
+                     bool have_prev, int pm0, int pn0) {
         constexpr bool EP = decltype(ep)::value;
         constexpr bool W24 = decltype(w24)::value;
         // ---- read segment: staging issue first (it does not wait for anything), then group 1's
         // counted wait, the previous tile's epilogue (its stores younger than every piece the
         // next waits count), the tile's bias slice, the fragment reads ----
-        stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value);
+        constexpr bool RF = RD1 && !EP && !decltype(first)::value;  // fragment reads before the staging
+        if constexpr (RF) reads(stc);
+        stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value,
+                     decltype(nxt)::value ? rot_n : rot_c);
+        hk.sub(ti, step);
         if constexpr (GRP == 1) {  // pieces of step t + 1 (issued two read segments ago) landed
             if (W24) vm_wait<24>(); else vm_wait<8>();
         }
         if constexpr (EP) {
+            hk.mark(ti, 0);
             if (have_prev) epilogue(pm0, pn0);
             else null_stores();
+            hk.mark(ti, 1);
         }
         if constexpr (decltype(first)::value) load_bias(n0);
-        reads(stc);
+        if constexpr (!RF) reads(stc);
         if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
-        bar();
+        bar(step, 0);
         // ---- MFMA segment ----
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the fragment reads (inline asm) landed
         __builtin_amdgcn_sched_barrier(0);
@@ -252,12 +320,15 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         if constexpr (GRP == 0) {
             if (W24) vm_wait<24>(); else vm_wait<8>();
         }
-        bar();
+        bar(step, 1);
     };
     // prologue: steps 0, 1, 2 of the first tile; the bias vector of the whole GEMM -> LDS
-    stage_pieces(rs_c, 0, 0);
-    stage_pieces(rs_c, 1, 1);
-    stage_pieces(rs_c, 2, 2);
+    auto rot_of = [&](int n0) { return ROT ? ((n0 / BN) & 3) * (nk >> 2) : 0; };
+    rot_c = rot_of(n0);
+    rot_n = rot_of(nn);
+    stage_pieces(rs_c, 0, 0, rot_c);
+    stage_pieces(rs_c, 1, 1, rot_c);
+    stage_pieces(rs_c, 2, 2, rot_c);
     {
         float* cv = (float*)(smem + 4 * STAGE);
         for (int i = (GRP * 256 + wc * 64 + lane); i < a.N; i += 512) cv[i] = a.bias ? a.bias[i] : 0.f;
@@ -280,43 +351,52 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     for (int i = 1;; ++i) {
         const bool have_prev = i > 1;
         // first group of four steps (0..3): step 0 carries the previous tile's epilogue
-        kstep(3, F_{}, S0{}, S3{}, T_{}, T_{}, W0{}, have_prev, pm0, pn0);
-        kstep(4, F_{}, S1{}, S0{}, F_{}, F_{}, T_{}, false, 0, 0);
-        kstep(5, F_{}, S2{}, S1{}, F_{}, F_{}, T_{}, false, 0, 0);
-        kstep(6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(0, 3, F_{}, S0{}, S3{}, T_{}, T_{}, W0{}, have_prev, pm0, pn0);
+        kstep(1, 4, F_{}, S1{}, S0{}, F_{}, F_{}, T_{}, false, 0, 0);
+        kstep(2, 5, F_{}, S2{}, S1{}, F_{}, F_{}, T_{}, false, 0, 0);
+        kstep(3, 6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
         for (int kt = 4; kt < nk - 4; kt += 4) {
-            kstep(kt + 3, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
-            kstep(kt + 4, F_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
-            kstep(kt + 5, F_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
-            kstep(kt + 6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt, kt + 3, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 1, kt + 4, F_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 2, kt + 5, F_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
+            kstep(kt + 3, kt + 6, F_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
         }
         // last group: steps nk - 4 .. nk - 1 stage nk - 1, then the next tile's steps 0, 1, 2
         // (nk >= 8: the launcher refuses K < 256)
-        kstep(nk - 1, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
-        kstep(0, T_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
-        kstep(1, T_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
-        kstep(2, T_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(nk - 4, nk - 1, F_{}, S0{}, S3{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(nk - 3, 0, T_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(nk - 2, 1, T_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
+        kstep(nk - 1, 2, T_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        ++ti;
         pm0 = m0;
         pn0 = n0;
         if (!has_next) break;
         m0 = mn;
         n0 = nn;
         rs_c = rs_n;
+        rot_c = rot_n;
         has_next = tile(i + 1, mn, nn);
+        rot_n = rot_of(nn);
         rs_n = has_next ? rsrc_of(mn, nn) : rs_none;
     }
+    hk.mark(ti, 0);
     epilogue(pm0, pn0);
+    hk.mark(ti, 1);
     if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
     vm_wait<0>();
 }
 
-template <typename T, int EPI, bool BLKA>
+template <typename T, int EPI, bool BLKA, bool BLKW = false, int STP = 0, class HK = P32Barrier, bool ROT = false,
+          int RES = 0, bool RD1 = false, int ABL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave < 4) p32_body<T, EPI, BLKA, 0>(a, ntiles, smem, lane, wave);
-    else p32_body<T, EPI, BLKA, 1>(a, ntiles, smem, lane, wave - 4);
+    HK hk;
+    hk.init(smem, lane, wave);
+    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, STP, 0, HK, ROT, RES, RD1, ABL>(a, ntiles, smem, lane, wave, hk);
+    else p32_body<T, EPI, BLKA, BLKW, STP, 1, HK, ROT, RES, RD1, ABL>(a, ntiles, smem, lane, wave - 4, hk);
+    hk.done(a);
 }
 
 }  // namespace clipvit

@@ -667,6 +667,23 @@ void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, i
     else pack_weight_kernel<BF16><<<blocks, threads, 0, s>>>(src, (u16*)dst, N, K, Kp);
 }
 
+// Row-major 16-bit [rows, cols] -> the 16-row blocked layout (blk16_off; rows % 16 == 0,
+// cols % 64 == 0): the weight operand of GEMM variant 73. One thread per 16-B chunk.
+__global__ void blk16_relayout_kernel(const uint4* __restrict__ src, unsigned char* __restrict__ dst, int rows,
+                                      int cols) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int cpr = cols >> 3;
+    if (idx >= (long)rows * cpr) return;
+    const int r = (int)(idx / cpr), c = (int)(idx % cpr);
+    *(uint4*)(dst + blk16_off(r, 8 * c, cols)) = src[idx];
+}
+
+void launch_blk16_relayout(hipStream_t s, const void* src, void* dst, int rows, int cols) {
+    const long total = (long)rows * (cols / 8);
+    blk16_relayout_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>((const uint4*)src, (unsigned char*)dst,
+                                                                         rows, cols);
+}
+
 // Uniform [-1, 1) 16-bit fill (benchmark operands: random data, not zeros, so the measured
 // clock is the one real inputs get — cdna_hip_programming.md §5.4 rule 25).
 template <typename T>

@@ -31,9 +31,10 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 62 the persistent 256x256 ping-pong tile
 # (gemm_pp.hip; 63 the same with non-temporal stores; 72 the 32-deep-k-step persistent tile of
-# gemm_p32.h);
+# gemm_p32.h); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472, 3480]
+VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472, 3480,
+            10008, 10022, 10072, 10080, 10081, 10082, 10090, 10098, 13472]
 N128 = (1, 2, 22, 81, 82)
 N256 = (3, 8, 62, 63, 72, 80, 98)
 STAGED = (62, 63, 72, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
@@ -76,7 +77,7 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("variant", STAGED + (8, 22))
+@pytest.mark.parametrize("variant", STAGED + (8, 22, 10072, 10081, 10098))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous

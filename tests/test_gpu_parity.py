@@ -416,3 +416,32 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
+
+
+@pytest.mark.parametrize("name,dtype,B,tun", [
+    ("ViT-B/32", "fp16", 256, {}),                            # QKV v98, c_fc tail v81 read the copy
+    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),   # 32-deep-k-step c_fc main
+    ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}),          # one launch per role, ragged M
+    ("ViT-B/16", "fp16", 64, {}),                             # N = 197, round split
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}),  # large-M pipelined tiles
+])
+def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun):
+    """QKV / c_fc weights read from their 16-row blocked copy (tuning w_blocked=1) move bytes
+    only: every tile computes the same products in the same order, so the features equal the
+    row-major run's bit for bit — after a LoRA merge, which re-packs both copies."""
+    cfg = C.get_config(name)
+    sd = synthetic_state_dict(cfg, 0)
+    ad = synthetic_adapters(cfg, rank=8)
+    px = _pixels(B, cfg.image_size, seed=53).to(gpu)
+    outs = []
+    for blk in (1, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk))
+        try:
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../ai-interior-image-classifier_amd/csrc/common.h"
+#include "../../ai-interior-image-classifier_amd/csrc/gemm_p32.h"
 
 using namespace clipvit;
 
@@ -327,6 +328,67 @@ __global__ __launch_bounds__(512, 1) void ppp_probe(GemmArgs a, int ntiles, unsi
     }
 }
 
+
+// ---- stamped barrier policy for variant 72 (gemm_p32.h): s_memtime on arrival at and departure
+// from every barrier of the first 3 tiles (24 k-steps each), and around the epilogue ----
+constexpr int P32_TILE = 24 * 5 + 4;  // per tile: [step][seg][arrive, depart], marks, [step] after-issue
+__device__ unsigned* g_p32_trace;
+struct P32Stamp {
+    unsigned* sbuf;
+    int lane, wave;
+    unsigned long long m0, r0;
+    __device__ void init(unsigned char* smem, int l, int w) {
+        sbuf = (unsigned*)(smem + 4 * 512 * 64) + 4096 + w * NST;
+        lane = l;
+        wave = w;
+        m0 = __builtin_amdgcn_s_memtime();
+        r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    __device__ void put(int idx, unsigned v) {
+        if (lane == 0) {
+            const unsigned a = (unsigned)(size_t)(LDS_AS unsigned*)(sbuf + idx);
+            asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+        }
+    }
+    __device__ void bar(int ti, int step, int seg) {
+        if (ti < 3 && step < 24) {
+            unsigned long long ta, td;
+            asm volatile("s_memtime %0\n\ts_barrier\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=&s"(ta), "=&s"(td)::"memory");
+            const int i = 8 + ti * P32_TILE + step * 4 + seg * 2;
+            put(i, (unsigned)ta);
+            put(i + 1, (unsigned)td);
+        } else {
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+    __device__ void sub(int ti, int step) {
+        if (ti < 3 && step < 24) {
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            put(8 + ti * P32_TILE + 100 + step, (unsigned)t);
+        }
+    }
+    __device__ void mark(int ti, int which) {
+        if (ti < 4 && ti >= 1) {
+            unsigned long long t;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            put(8 + (ti - 1) * P32_TILE + 96 + which, (unsigned)t);
+        }
+    }
+    __device__ void done(const GemmArgs&) {
+        const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();
+        unsigned* out = g_p32_trace + ((size_t)blockIdx.x * 8 + wave) * NST;
+        for (int i = 8 + lane; i < NST; i += 64) out[i] = sbuf[i];
+        if (lane == 0) {
+            out[0] = (unsigned)m0; out[1] = (unsigned)(m0 >> 32);
+            out[2] = (unsigned)r0; out[3] = (unsigned)(r0 >> 32);
+            out[4] = (unsigned)m1; out[5] = (unsigned)(m1 >> 32);
+            out[6] = (unsigned)r1; out[7] = (unsigned)(r1 >> 32);
+        }
+    }
+};
+
 // ---- host ----
 __global__ void fill_f16(u16* p, size_t n, unsigned seed) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -427,7 +489,10 @@ static void bar_case(const char* name, int iters) {
 // 8 waves, waves 4-7 one barrier late; per iteration every wave runs [read segment: NREAD
 // ds_read_b128 + NDMA buffer_load ... lds pieces (L2-resident source), vmcnt keeping two segments
 // in flight] barrier [lgkmcnt(0), MPS MFMAs on the fragments just read] barrier.
-template <int MPS, int NDMA, int NREAD>
+// SRC: 0 = every workgroup reads the same 1 MB window (L2 hits), 1 KB contiguous per piece;
+// 1 = each workgroup streams its own 1 MB (256 MB in all: L2 misses); 2 / 3 = the same with the
+// row-major operand pattern of gemm_p32 (16 rows x 64 B per piece, rows 1536 B apart)
+template <int MPS, int NDMA, int NREAD, int SRC = 0>
 __global__ __launch_bounds__(512, 1) void pp_seg_probe(const unsigned char* src, float* out, unsigned* cyc, int iters) {
     typedef F16::vec8 vec8;
     __shared__ __attribute__((aligned(16))) unsigned char smem[160 * 1024];
@@ -436,8 +501,9 @@ __global__ __launch_bounds__(512, 1) void pp_seg_probe(const unsigned char* src,
     const int grp = wave >> 2;
     for (int i = threadIdx.x; i < 160 * 1024 / 4; i += 512) ((float*)smem)[i] = 0.001f * (i & 255);
     __syncthreads();
-    const i32x4_t rs = buf_rsrc(src, 2u << 20);
-    const unsigned voff = (unsigned)(wave * 1024 + lane * 16);
+    const i32x4_t rs = buf_rsrc(src + ((SRC & 1) ? (size_t)blockIdx.x * (2u << 20) : 0), 2u << 20);
+    const unsigned voff = (SRC & 2) ? (unsigned)((16 * wave + (lane >> 2)) * 1536 + (lane & 3) * 16)
+                                    : (unsigned)(wave * 1024 + lane * 16);
     constexpr int NR = NREAD > 0 ? NREAD : 1;
     vec8 fr[NR];
     vec8 b;
@@ -453,7 +519,9 @@ __global__ __launch_bounds__(512, 1) void pp_seg_probe(const unsigned char* src,
             fr[r] = *(const vec8*)(smem + 65536 + ((wave * NREAD + r) * 1024 + lane * 16) % 65536);
 #pragma unroll
         for (int d = 0; d < NDMA; ++d)
-            blds16(rs, voff, ((it * NDMA + d) * 8192) & ((1 << 20) - 1), smem + ((d * 8 + wave) * 1024) % 65536);
+            blds16(rs, voff, (SRC & 2) ? ((it * NDMA + d) & 31) * 64 + (((it * NDMA + d) >> 5) & 3) * 196608
+                                       : ((it * NDMA + d) * 8192) & ((1 << 20) - 1),
+                   smem + ((d * 8 + wave) * 1024) % 65536);
         if constexpr (NDMA > 0) vm_wait<2 * NDMA>();
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -477,20 +545,20 @@ __global__ __launch_bounds__(512, 1) void pp_seg_probe(const unsigned char* src,
     if (lane == 0) cyc[blockIdx.x * 8 + wave] = (unsigned)(t1 - t0);
 }
 
-template <int MPS, int NDMA, int NREAD>
+template <int MPS, int NDMA, int NREAD, int SRC = 0>
 static void seg_case(const unsigned char* src, int iters) {
     float* out;
     unsigned* cyc;
     CK(hipMalloc(&out, 256 * 512 * 4));
     CK(hipMalloc(&cyc, 256 * 8 * 4));
-    for (int r = 0; r < 3; ++r) pp_seg_probe<MPS, NDMA, NREAD><<<256, 512>>>(src, out, cyc, iters);
+    for (int r = 0; r < 3; ++r) pp_seg_probe<MPS, NDMA, NREAD, SRC><<<256, 512>>>(src, out, cyc, iters);
     CK(hipDeviceSynchronize());
     std::vector<unsigned> c(256 * 8);
     CK(hipMemcpy(c.data(), cyc, c.size() * 4, hipMemcpyDeviceToHost));
     std::sort(c.begin(), c.end());
     const double per_int = (double)c[c.size() / 2] / iters / 2;  // two intervals per iteration
-    printf("segment: %3d MFMA | partner %2d ds_read_b128 + %d LDS-DMA: %6.1f cyc per interval (MFMA %d, busy %.2f)\n", MPS,
-           NREAD, NDMA, per_int, MPS * 16, MPS * 16 / per_int);
+    printf("segment: %3d MFMA | partner %2d ds_read_b128 + %d LDS-DMA (src %d): %6.1f cyc per interval (MFMA %d, busy %.2f)\n",
+           MPS, NREAD, NDMA, SRC, per_int, MPS * 16, MPS * 16 / per_int);
     CK(hipFree(out));
     CK(hipFree(cyc));
 }
@@ -524,8 +592,8 @@ int main(int argc, char** argv) {
         bar_case<4, 64, 1>("4 waves, 64 MFMA then barrier", 500);
         bar_case<4, 128, 1>("4 waves, 128 MFMA then barrier", 250);
         unsigned char* src;
-        CK(hipMalloc(&src, 4 << 20));
-        CK(hipMemset(src, 0, 4 << 20));
+        CK(hipMalloc(&src, (size_t)512 << 20));
+        CK(hipMemset(src, 0, (size_t)512 << 20));
         seg_case<16, 0, 0>(src, 2000);
         seg_case<16, 0, 4>(src, 2000);
         seg_case<16, 0, 8>(src, 2000);
@@ -543,6 +611,185 @@ int main(int argc, char** argv) {
         seg_case<0, 2, 8>(src, 2000);
         seg_case<0, 2, 0>(src, 2000);
         seg_case<0, 0, 8>(src, 2000);
+        // v72's segment against the source pattern
+        seg_case<32, 4, 12, 0>(src, 1000);
+        seg_case<32, 4, 12, 1>(src, 1000);
+        seg_case<32, 4, 12, 2>(src, 1000);
+        seg_case<32, 4, 12, 3>(src, 1000);
+        seg_case<0, 4, 12, 0>(src, 1000);
+        seg_case<0, 4, 12, 1>(src, 1000);
+        seg_case<0, 4, 12, 3>(src, 1000);
+        seg_case<16, 2, 12, 1>(src, 2000);
+        seg_case<16, 2, 12, 3>(src, 2000);
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "p32run") {  // p32run M N K epi xcd iters kind (PMC passes)
+        const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), epi = atoi(argv[5]), xcd = atoi(argv[6]);
+        const int iters = atoi(argv[7]), kind = argc > 8 ? atoi(argv[8]) : 0;  // 0 v72, 1 v72 blocked A + W, 2 v62
+        u16 *A, *W, *C;
+        float* bias;
+        CK(hipMalloc(&A, (size_t)(M + 256) * K * 2));
+        CK(hipMalloc(&W, (size_t)N * K * 2));
+        CK(hipMalloc(&C, (size_t)M * N * 2));
+        CK(hipMalloc(&bias, (size_t)N * 4));
+        fill_f16<<<1024, 256>>>(A, (size_t)(M + 256) * K, 1);
+        fill_f16<<<1024, 256>>>(W, (size_t)N * K, 2);
+        CK(hipMemset(bias, 0, N * 4));
+        GemmArgs a{};
+        a.A = A; a.W = W; a.bias = bias; a.C = C;
+        a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd;
+        const int ntiles = ((M + 255) / 256) * (N / 256), grid = std::min(ntiles, 256);
+        for (int i = 0; i < iters; ++i) {
+            if (kind == 2) {
+                if (epi) ppp_probe<F16, EPI_GELU, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
+                else ppp_probe<F16, EPI_STORE, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
+            } else if (kind == 1) {
+                if (epi) gemm_p32_kernel<F16, EPI_GELU, true, true><<<grid, 512>>>(a, ntiles);
+                else gemm_p32_kernel<F16, EPI_STORE, true, true><<<grid, 512>>>(a, ntiles);
+            } else {
+                if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles);
+                else gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles);
+            }
+        }
+        CK(hipDeviceSynchronize());
+        printf("p32run done\n");
+        return 0;
+    }
+    if (argc > 1 && std::string(argv[1]) == "p32") {  // p32 M N K epi xcd: operand layout experiment
+        const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), epi = atoi(argv[5]), xcd = atoi(argv[6]);
+        u16 *A, *W, *C;
+        float* bias;
+        CK(hipMalloc(&A, (size_t)(M + 256) * K * 2));
+        CK(hipMalloc(&W, (size_t)N * K * 2));
+        CK(hipMalloc(&C, (size_t)M * N * 2));
+        CK(hipMalloc(&bias, (size_t)N * 4));
+        fill_f16<<<1024, 256>>>(A, (size_t)(M + 256) * K, 1);
+        fill_f16<<<1024, 256>>>(W, (size_t)N * K, 2);
+        CK(hipMemset(bias, 0, N * 4));
+        GemmArgs a{};
+        a.A = A; a.W = W; a.bias = bias; a.C = C;
+        a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd;
+        const int ntiles = ((M + 255) / 256) * (N / 256), grid = std::min(ntiles, 256);
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        auto run = [&](const char* name, auto fn) {
+            for (int i = 0; i < 5; ++i) fn();
+            float best = 1e9f;
+            for (int r = 0; r < 5; ++r) {
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < 20; ++i) fn();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = std::min(best, ms / 20);
+            }
+            printf("%-40s %7.2f us  %.0f TF/s\n", name, best * 1e3, 2.0 * M * N * K / (best * 1e-3) / 1e12);
+        };
+        // stamped run of the default layout after 2 s of plain launches
+        {
+            unsigned* tr;
+            CK(hipMalloc(&tr, (size_t)grid * 8 * NST * 4));
+            CK(hipMemset(tr, 0, (size_t)grid * 8 * NST * 4));
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p32_trace), &tr, sizeof(tr)));
+            CK(hipEventRecord(e0));
+            float ms = 0.f;
+            while (ms < 2000.f) {
+                for (int i = 0; i < 100; ++i) {
+                    if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles);
+                    else gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles);
+                }
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms, e0, e1));
+            }
+            if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false, 0, P32Stamp><<<grid, 512>>>(a, ntiles);
+            else gemm_p32_kernel<F16, EPI_STORE, false, false, 0, P32Stamp><<<grid, 512>>>(a, ntiles);
+            CK(hipDeviceSynchronize());
+            std::vector<unsigned> t((size_t)grid * 8 * NST);
+            CK(hipMemcpy(t.data(), tr, t.size() * 4, hipMemcpyDeviceToHost));
+            auto u64 = [&](const unsigned* p, int i) { return (unsigned long long)p[i] | ((unsigned long long)p[i + 1] << 32); };
+            auto med = [](std::vector<double>& v) { std::sort(v.begin(), v.end()); return v.empty() ? -1.0 : v[v.size() / 2]; };
+            std::vector<double> clk, span;
+            for (int g = 0; g < grid; ++g) {
+                const unsigned* p = &t[(size_t)g * 8 * NST];
+                clk.push_back((double)(u64(p, 4) - u64(p, 0)) / (double)(u64(p, 6) - u64(p, 2)) * 0.1);
+                span.push_back((double)(u64(p, 6) - u64(p, 2)) * 0.01);
+            }
+            printf("stamped p32: in-kernel clock %.3f GHz (median), workgroup span %.2f us (median)\n", med(clk), med(span));
+            const int nks = std::min(K / 32, 24);
+            for (int tix = 0; tix < 2; ++tix)
+                for (int wv : {0, 4}) {
+                    printf("tile %d wave %d: per k-step [read seg work/wait | MFMA seg work/wait] cycles\n", tix, wv);
+                    double sr = 0, sm = 0, sx = 0;
+                    int nn = 0;
+                    for (int st = 0; st < nks; ++st) {
+                        double v4[4];
+                        for (int seg = 0; seg < 2; ++seg) {
+                            std::vector<double> w, x;
+                            for (int g = 0; g < grid; ++g) {
+                                const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
+                                const int i = 8 + tix * P32_TILE + st * 4 + seg * 2;
+                                const int dprev = seg == 1 ? i - 1 : (st > 0 ? i - 3 : -1);
+                                if (!p[i] || !p[i + 1]) continue;
+                                x.push_back((double)(unsigned)(p[i + 1] - p[i]));
+                                if (dprev >= 0 && p[dprev]) w.push_back((double)(unsigned)(p[i] - p[dprev]));
+                            }
+                            v4[2 * seg] = med(w);
+                            v4[2 * seg + 1] = med(x);
+                        }
+                        std::vector<double> is;
+                        for (int g = 0; g < grid; ++g) {
+                            const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
+                            const int i = 8 + tix * P32_TILE + st * 4;
+                            const unsigned su = p[8 + tix * P32_TILE + 100 + st];
+                            if (st > 0 && su && p[i - 1]) is.push_back((double)(unsigned)(su - p[i - 1]));
+                        }
+                        const double iss = med(is);
+                        if (st < 4 || st >= nks - 2 || st == nks / 2)
+                            printf("  step %2d: R %5.0f/%-5.0f (staging issue %5.0f) | M %5.0f/%-5.0f\n", st, v4[0], v4[1], iss, v4[2], v4[3]);
+                        if (st >= 4 && st < nks - 1) { sr += v4[0]; sm += v4[2]; sx += v4[1] + v4[3]; ++nn; }
+                    }
+                    if (nn) printf("  steady (steps 4..%d): R work %.0f + M work %.0f + waits %.0f = %.0f cyc per k-step\n", nks - 2, sr / nn, sm / nn, sx / nn, (sr + sm + sx) / nn);
+                    std::vector<double> ep;
+                    for (int g = 0; g < grid; ++g) {
+                        const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
+                        const int i = 8 + tix * P32_TILE + 96;
+                        if (p[i] && p[i + 1]) ep.push_back((double)(unsigned)(p[i + 1] - p[i]));
+                    }
+                    printf("  epilogue of this tile (in the next tile's first read segment): %.0f cyc (n=%zu)\n", med(ep), ep.size());
+                }
+            CK(hipFree(tr));
+        }
+        for (int rep = 0; rep < 2; ++rep) {
+            if (epi) {
+                run("p32 A row-major, W row-major", [&] { gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles); });
+                run("p32 A blocked,   W row-major", [&] { gemm_p32_kernel<F16, EPI_GELU, true, false><<<grid, 512>>>(a, ntiles); });
+                run("p32 A row-major, W blocked", [&] { gemm_p32_kernel<F16, EPI_GELU, false, true><<<grid, 512>>>(a, ntiles); });
+                run("p32 A blocked,   W blocked", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true><<<grid, 512>>>(a, ntiles); });
+            } else {
+                run("p32 A row-major, W row-major", [&] { gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles); });
+                run("p32 A blocked,   W row-major", [&] { gemm_p32_kernel<F16, EPI_STORE, true, false><<<grid, 512>>>(a, ntiles); });
+                run("p32 A row-major, W blocked", [&] { gemm_p32_kernel<F16, EPI_STORE, false, true><<<grid, 512>>>(a, ntiles); });
+                run("p32 A blocked,   W blocked", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true><<<grid, 512>>>(a, ntiles); });
+            }
+            if (epi) {
+                run("p32 blocked: no staging", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 7><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no MFMA", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 8><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no fragment reads", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 9><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no stores", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 3><<<grid, 512>>>(a, ntiles); });
+            } else {
+                run("p32 blocked: no staging", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 7><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no MFMA", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 8><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no fragment reads", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 9><<<grid, 512>>>(a, ntiles); });
+                run("p32 blocked: no stores", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 3><<<grid, 512>>>(a, ntiles); });
+            }
+            run("v62 copy (ppp_probe)", [&] {
+                if (epi) ppp_probe<F16, EPI_GELU, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
+                else ppp_probe<F16, EPI_STORE, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
+            });
+        }
         return 0;
     }
     if (argc < 6) {

@@ -10,3 +10,7 @@ tail -2 $out/tests.log
 timeout -k 10 300 python -u tools/gemm_ab.py "10752,3072,768,1;12800,3072,768,1;12800,2304,768,0;4096,4096,4096,0" \
   "3462,3472,62,72" 5 20 > $out/ab.log 2>&1 || { echo "ab failed"; tail -20 $out/ab.log; exit 1; }
 cat $out/ab.log
+# in-model: the shipped line against v72 as the c_fc main launch, and also as the QKV tile
+bash tools/ab_envs.sh "--steps 20 --warmup 5" 2 - "--tuning split_variants=72,81" \
+  "--tuning split_variants=72,81;qkv_variant=72" > $out/inmodel.log 2>&1 || { echo "in-model A/B failed"; tail -20 $out/inmodel.log; exit 1; }
+cat $out/inmodel.log
