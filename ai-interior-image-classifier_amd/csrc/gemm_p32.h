@@ -64,7 +64,7 @@ __device__ void p32_store16(u32x4 vdata, i32x4_t rsrc, int voffset, int soffset,
 // RES (diagnostic, outputs garbage): 1 = every tile stages the first W panel, 2 = the first A
 // panel, so that operand is an L2 hit after its first fetch
 // ABL (diagnostic, outputs garbage): 7 = no staging after the prologue, 8 = no MFMA, 9 = no
-// fragment reads, 3 = no epilogue stores
+// fragment reads, 3 = no epilogue stores, 4 = row-major stores into rows m & 255 only
 template <typename T, int EPI, bool BLKA, bool BLKW, int STP, int GRP, class HK, bool ROT = false, int RES = 0,
           bool RD1 = false, int ABL = 0>
 __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
@@ -246,7 +246,8 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                     w1[d] = r[1];
                 }
                 const int g = le >> 4;
-                off = ((size_t)m * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
+                const int ms = ABL == 4 ? (m & 255) : m;  // (ABL 4: every tile's rows alias one L2-resident band)
+                off = ((size_t)ms * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
                 off2 = off + 64;
             }
             if (m < a.M && (ABL != 3 || a.ldc < 0)) {
