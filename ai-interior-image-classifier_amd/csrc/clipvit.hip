@@ -232,9 +232,10 @@ struct clipvit_handle {
     bool x16 = true;
     // 16-bit forward (fp16 / bf16), 24-bit residual stream: x between the LayerNorm kernels as
     // 16 + 8 bit planes (norm.hip x24_load) instead of fp32: the add + LayerNorm kernels move 3
-    // bytes per element of x instead of 4 (tuning x24=0: fp32 x)
+    // bytes per element of x instead of 4 (tuning x24=0: fp32 x). With lnfold the planes are read
+    // and written by the residual producers' EPI_RES_STATS epilogues (GemmArgs.x24_plane)
     bool x24 = true;
-    bool use_x24() const { return x24 && !mx8 && !lnfold && resid16 && defer_x && cls_prune; }
+    bool use_x24() const { return x24 && !mx8 && cls_prune && (lnfold || (resid16 && defer_x)); }
     bool use_x16() const {
         return x16 && mx8 && resid16 && defer_x && cls_prune && ((mx8_skip >> (cfg.layers - 1)) & 1) &&
                ((mx8_skip_mlp >> (cfg.layers - 1)) & 1);
@@ -408,6 +409,7 @@ struct Fold {
     float2* st_out = nullptr;
     void* C2 = nullptr;
     int np = 0;
+    size_t x24_plane = 0;  // EPI_RES_STATS: C = the 24-bit residual planes (GemmArgs.x24_plane)
 };
 
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
@@ -417,6 +419,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
     a.lnf_s = fo.s; a.st_in = fo.st_in; a.st_out = fo.st_out; a.C2 = fo.C2; a.np = fo.np;
+    a.x24_plane = fo.x24_plane;
     a.patch_g2 = h->G2; a.patch_ntok = h->N;
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
@@ -731,7 +734,8 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
 // out_proj tile (160x128, EPI_RES_STATS: x += ., x16, the 128-column statistics in the same
 // order), c_fc with the folded ln_2, c_proj (+x, fp32) — so the features equal the unpruned
 // forward's bit for bit; then ln_post @ proj.
-static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof) {
+static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof,
+                         const void* x24 = nullptr) {
     const int D = h->D, N = h->N, np = D / 128;
     const LayerW& ly = h->layers[h->cfg.layers - 1];
     unsigned char* base = (unsigned char*)w->u;
@@ -740,7 +744,7 @@ static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float
     u16* yc = hc + (size_t)B * D;
     u16* uc = yc + (size_t)B * D;
     float2* sc = (float2*)(uc + (size_t)B * 4 * D);
-    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D);
+    launch_gather_cls(s, w->x, w->h, xc, hc, B, N, D, x24, x24 != nullptr);
     auto g0 = [&](int epi, int variant, const void* A, const void* W, const float* bias, void* C, int n, int k,
                   const Fold& fo) {
         GemmArgs a{};
@@ -783,7 +787,10 @@ static int forward_fold(clipvit_handle* h, hipStream_t s, const void* pix, int i
     int rc;
     if (prof) prof->mark(s, F_EMBED);
     if ((rc = patch_embed(h, s, pix, in_dtype, B, w))) return rc;
-    launch_embed_stats(s, h->dt, w->x, w->h, w->st, h->cls, h->pos, h->lnpre_g, h->lnpre_b, B, N, D);
+    // X24: the residual stream in 24-bit planes (w->x then only holds the patch GEMM's rows)
+    void* X24 = h->use_x24() ? w->x16 : nullptr;
+    const size_t plane = (size_t)M * D * 2;
+    launch_embed_stats(s, h->dt, w->x, w->h, w->st, h->cls, h->pos, h->lnpre_g, h->lnpre_b, B, N, D, X24);
     if (prof) prof->mark(s, F_EMBED);
     void* x16b = w->qkv;  // x16 after out_proj (qkv is dead once attention has read it)
     const int nl = h->cfg.layers;
@@ -796,21 +803,22 @@ static int forward_fold(clipvit_handle* h, hipStream_t s, const void* pix, int i
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
         if (prof) prof->mark(s, F_ATTN);
         if (i + 1 == nl && h->cls_prune) {
-            if ((rc = cls_tail_fold(h, s, B, w, f_out, prof))) return rc;
+            if ((rc = cls_tail_fold(h, s, B, w, f_out, prof, X24))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
         }
         Fold fo;
-        fo.st_out = w->st; fo.C2 = x16b; fo.np = np;
-        if ((rc = gemm(s, h, EPI_RES_STATS, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT, fo))) return rc;
+        fo.st_out = w->st; fo.C2 = x16b; fo.np = np; fo.x24_plane = X24 ? plane : 0;
+        void* xres = X24 ? X24 : (void*)w->x;
+        if ((rc = gemm(s, h, EPI_RES_STATS, w->h, ly.wout, ly.bout, xres, M, D, D, D, R_OUT, fo))) return rc;
         if (prof) prof->mark(s, F_OUT);
         Fold ff;
         ff.s = ly.s_fc; ff.st_in = w->st; ff.np = np;
         if ((rc = gemm(s, h, EPI_LNF_GELU, x16b, ly.wfc, ly.bf_fc, w->u, M, 4 * D, D, 4 * D, R_FC, ff))) return rc;
         if (prof) prof->mark(s, F_FC);
         Fold fp;
-        fp.st_out = w->st; fp.C2 = w->h; fp.np = np;
-        if ((rc = gemm(s, h, EPI_RES_STATS, w->u, ly.wproj, ly.bproj, w->x, M, D, 4 * D, D, R_PROJ, fp))) return rc;
+        fp.st_out = w->st; fp.C2 = w->h; fp.np = np; fp.x24_plane = fo.x24_plane;
+        if ((rc = gemm(s, h, EPI_RES_STATS, w->u, ly.wproj, ly.bproj, xres, M, D, 4 * D, D, R_PROJ, fp))) return rc;
         if (prof) prof->mark(s, F_PROJ);
     }
     launch_cls_ln_proj(s, w->x, h->lnpost_g, h->lnpost_b, h->proj, f_out, B, N, D, h->E, h->head_cols);

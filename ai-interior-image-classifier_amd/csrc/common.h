@@ -185,6 +185,9 @@ struct GemmArgs {
     // 64-deep k-tile of 16 weight rows is one contiguous 2 KB run. Pipelined tiles (8..98, not the
     // patch GEMM) and the 32-deep-k-step persistent tile (72) only.
     int blk_w;
+    // EPI_RES_STATS: the residual x in 24-bit planes (x24_load / x24_store: C = the [M][ldc] u16
+    // high plane, the byte plane at C + x24_plane); 0 = fp32 x at C
+    size_t x24_plane;
 };
 
 // 16-row blocked layout of a 16-bit [rows, ncols] matrix (ncols % 64 == 0): 16 x 64 blocks of
@@ -202,6 +205,26 @@ __host__ __device__ inline size_t blk16_off(int m, int f, int ncols) {
 __host__ __device__ inline size_t blk8_off(int m, int f, int ncols) {
     return ((((size_t)(m >> 4) * (size_t)(ncols >> 7)) + (size_t)(f >> 7)) << 11) + (size_t)(((f & 127) >> 4) << 8) +
            (size_t)((m & 15) << 4) + (size_t)(f & 15);
+}
+
+// 24-bit residual rows (X24, the 16-bit forward): x as two planes, hi = the upper 16 bits of
+// each fp32 value ([rows][D] u16 at base) and lo = the next 8 ([rows][D] bytes at base + plane),
+// rounded to nearest at bit 8: a 16-bit significand (relative error <= 2^-16, against 2^-11 for
+// the 16-bit GEMM operands), 3 bytes per element instead of 4. idx = row * D + column (4-aligned).
+__device__ __forceinline__ float4 x24_load(const unsigned char* base, size_t plane, size_t idx) {
+    const uint2 hi = *(const uint2*)(base + idx * 2);
+    const unsigned lo = *(const unsigned*)(base + plane + idx);
+    return make_float4(__uint_as_float((hi.x << 16) | ((lo & 0xffu) << 8)),
+                       __uint_as_float((hi.x & 0xffff0000u) | (lo & 0xff00u)),
+                       __uint_as_float((hi.y << 16) | ((lo >> 8) & 0xff00u)),
+                       __uint_as_float((hi.y & 0xffff0000u) | ((lo >> 16) & 0xff00u)));
+}
+__device__ __forceinline__ void x24_store(unsigned char* base, size_t plane, size_t idx, float4 v) {
+    const unsigned a = __float_as_uint(v.x) + 0x80u, b = __float_as_uint(v.y) + 0x80u;
+    const unsigned c = __float_as_uint(v.z) + 0x80u, d = __float_as_uint(v.w) + 0x80u;
+    *(uint2*)(base + idx * 2) = make_uint2((a >> 16) | (b & 0xffff0000u), (c >> 16) | (d & 0xffff0000u));
+    *(unsigned*)(base + plane + idx) =
+        ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c << 8) & 0xff0000u) | ((d << 16) & 0xff000000u);
 }
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,
@@ -367,9 +390,10 @@ void launch_widen16(hipStream_t s, int dtype, const void* src, float* dst, size_
 void launch_lnfold_prep(hipStream_t s, int dtype, const float* W, const float* gamma, const float* beta,
                         const float* b, float* Wg, float* s_out, float* b_out, int N, int K);
 // embedding for the folded path: x = ln_pre(cls / patch + pos); x16 = x (16-bit); st = 128-col
-// partial (mean, M2) of x
+// partial (mean, M2) of x; x24 (not null): x stored in the 24-bit planes there
 void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* st, const float* cls,
-                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D);
+                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D,
+                        void* x24 = nullptr);
 
 
 int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,

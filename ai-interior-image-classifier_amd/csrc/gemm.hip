@@ -231,7 +231,9 @@ __device__ __forceinline__ void lnf_apply(float (&v)[16], const float* __restric
 }
 
 // EPI_RES_STATS (residual producers out_proj / c_proj): x += acc + bias (fp32, the same additions
-// as EPI_RESID), x16 = x, and per row the (mean, M2) of x over each 128-column group = two
+// as EPI_RESID; x read and written as fp32 or, with a.x24_plane, as the 24-bit planes: the sum is
+// rounded to 24 bits only where it is stored, as launch_add_layernorm_deferred does), x16 = x
+// (16-bit, of the fp32 sum), and per row the (mean, M2) of the fp32 sum over each 128-column group = two
 // adjacent 64-column waves (TN == 64): the 64-column sums are shuffle-reduced over the 4 lanes of
 // a row, exchanged with the partner wave through LDS, then the squared deviations from the
 // group mean the same way (two-pass, no cancellation).
@@ -251,12 +253,16 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
     for (int fm = 0; fm < FM; ++fm) {
         const int m = m0 + wm * TM + fm * 16 + lrow;
         const int n = n0 + wn * TN + 16 * g;
-        float* xr = (float*)a.C + (size_t)min(m, a.M - 1) * a.ldc + n;
+        const size_t xi = (size_t)min(m, a.M - 1) * a.ldc + n;  // x element index (fp32 or 24-bit planes)
+        float* xr = (float*)a.C + xi;
+        unsigned char* const xb = (unsigned char*)a.C;
         const float4* b4 = (const float4*)bias;
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const float4 bb = b4[i], xo = PREX ? xpre[PREX ? fm : 0][i] : ((const float4*)xr)[i];
+            const float4 bb = b4[i];
+            const float4 xo = PREX ? xpre[PREX ? fm : 0][i]
+                                   : (a.x24_plane ? x24_load(xb, a.x24_plane, xi + 4 * i) : ((const float4*)xr)[i]);
             f32x4& c = acc[i][fm];
             c[0] = xo.x + (c[0] + bb.x);
             c[1] = xo.y + (c[1] + bb.y);
@@ -266,8 +272,15 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
         }
         if (m < a.M) {
             unsigned char* hr = (unsigned char*)a.C2 + ((size_t)m * a.ldc + n) * 2;
+            if (a.x24_plane) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ((float4*)xr)[i] = make_float4(acc[i][fm][0], acc[i][fm][1], acc[i][fm][2], acc[i][fm][3]);
+                for (int i = 0; i < 4; ++i)
+                    x24_store(xb, a.x24_plane, xi + 4 * i, make_float4(acc[i][fm][0], acc[i][fm][1], acc[i][fm][2], acc[i][fm][3]));
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    ((float4*)xr)[i] = make_float4(acc[i][fm][0], acc[i][fm][1], acc[i][fm][2], acc[i][fm][3]);
+            }
             *(uint4*)hr = make_uint4(pack2<T>(acc[0][fm][0], acc[0][fm][1]), pack2<T>(acc[0][fm][2], acc[0][fm][3]),
                                      pack2<T>(acc[1][fm][0], acc[1][fm][1]), pack2<T>(acc[1][fm][2], acc[1][fm][3]));
             *(uint4*)(hr + 16) = make_uint4(pack2<T>(acc[2][fm][0], acc[2][fm][1]), pack2<T>(acc[2][fm][2], acc[2][fm][3]),
@@ -580,9 +593,15 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
 #pragma unroll
             for (int fm = 0; fm < FM; ++fm) {
                 const int m = min(m0 + wm * TM + fm * 16 + lrow, mlast);
-                const float4* xr = (const float4*)((const float*)a.C + (size_t)m * a.ldc + n0 + wn * TN + 16 * lg);
+                const size_t idx = (size_t)m * a.ldc + n0 + wn * TN + 16 * lg;
+                if (a.x24_plane) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) xpre[fm][i] = xr[i];
+                    for (int i = 0; i < 4; ++i) xpre[fm][i] = x24_load((const unsigned char*)a.C, a.x24_plane, idx + 4 * i);
+                } else {
+                    const float4* xr = (const float4*)((const float*)a.C + idx);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) xpre[fm][i] = xr[i];
+                }
             }
         }
         mfmas(a0, w0);

@@ -128,25 +128,7 @@ __device__ __forceinline__ float4 unpack4_f16(uint2 w) {
                        F16::to_f32((u16)(w.y & 0xffff)), F16::to_f32((u16)(w.y >> 16)));
 }
 
-// 24-bit residual rows (X24, the 16-bit forward): x as two planes, hi = the upper 16 bits of
-// each fp32 value ([rows][D] u16 at base) and lo = the next 8 ([rows][D] bytes at base + plane),
-// rounded to nearest at bit 8: a 16-bit significand (relative error <= 2^-16, against 2^-11 for
-// the 16-bit GEMM operands), 3 bytes per element instead of 4. idx = row * D + column (4-aligned).
-__device__ __forceinline__ float4 x24_load(const unsigned char* base, size_t plane, size_t idx) {
-    const uint2 hi = *(const uint2*)(base + idx * 2);
-    const unsigned lo = *(const unsigned*)(base + plane + idx);
-    return make_float4(__uint_as_float((hi.x << 16) | ((lo & 0xffu) << 8)),
-                       __uint_as_float((hi.x & 0xffff0000u) | (lo & 0xff00u)),
-                       __uint_as_float((hi.y << 16) | ((lo >> 8) & 0xff00u)),
-                       __uint_as_float((hi.y & 0xffff0000u) | ((lo >> 16) & 0xff00u)));
-}
-__device__ __forceinline__ void x24_store(unsigned char* base, size_t plane, size_t idx, float4 v) {
-    const unsigned a = __float_as_uint(v.x) + 0x80u, b = __float_as_uint(v.y) + 0x80u;
-    const unsigned c = __float_as_uint(v.z) + 0x80u, d = __float_as_uint(v.w) + 0x80u;
-    *(uint2*)(base + idx * 2) = make_uint2((a >> 16) | (b & 0xffff0000u), (c >> 16) | (d & 0xffff0000u));
-    *(unsigned*)(base + plane + idx) =
-        ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c << 8) & 0xff0000u) | ((d << 16) & 0xff000000u);
-}
+// 24-bit residual rows (X24): x24_load / x24_store, common.h.
 
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
@@ -234,12 +216,14 @@ __device__ __forceinline__ void row_stats128(const float4 (&v)[V], float2* __res
 }
 
 // x[row] = ln_pre((t == 0 ? class_embedding : patch_row) + pos[t]); x16[row] = x[row] (16-bit);
-// st[row] = its 128-column statistics (block 0's ln_1 is folded into the QKV GEMM)
+// st[row] = its 128-column statistics (block 0's ln_1 is folded into the QKV GEMM). x24 (not
+// null): x is stored in the 24-bit planes there instead (x keeps the patch rows it was read from)
 template <typename T, int V>
 __global__ __launch_bounds__(256) void embed_stats_kernel(float* __restrict__ x, u16* __restrict__ x16,
                                                           float2* __restrict__ st, const float* __restrict__ cls,
                                                           const float* __restrict__ pos, const float* __restrict__ gp,
-                                                          const float* __restrict__ bp, int rows, int N) {
+                                                          const float* __restrict__ bp, int rows, int N,
+                                                          unsigned char* __restrict__ x24) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= rows) return;
@@ -256,8 +240,13 @@ __global__ __launch_bounds__(256) void embed_stats_kernel(float* __restrict__ x,
         v[i] = make_float4(a.x + p.x, a.y + p.y, a.z + p.z, a.w + p.w);
     }
     ln_row<V>(v, gp, bp, lane, (float)D);
+    if (x24) {
 #pragma unroll
-    for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+        for (int i = 0; i < V; ++i) x24_store(x24, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4, v[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) *(float4*)(xr + (lane + 64 * i) * 4) = v[i];
+    }
     store_row16<T, V>(x16 + (size_t)row * D, v, lane);
     row_stats128<V>(v, st + (size_t)row * (D / 128), lane);
 }
@@ -487,13 +476,14 @@ void launch_embed_ln_q8(hipStream_t s, float* x, unsigned char* q, unsigned char
 }
 
 void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* st, const float* cls,
-                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D) {
+                        const float* pos, const float* g_pre, const float* b_pre, int B, int N, int D, void* x24) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
+    unsigned char* x24b = (unsigned char*)x24;
     if (dtype == 2) {
-        DISPATCH_V(D, embed_stats_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N));
+        DISPATCH_V(D, embed_stats_kernel<F16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N, x24b));
     } else {
-        DISPATCH_V(D, embed_stats_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N));
+        DISPATCH_V(D, embed_stats_kernel<BF16, V><<<grid, block, 0, s>>>(x, (u16*)x16, st, cls, pos, g_pre, b_pre, rows, N, x24b));
     }
 }
 

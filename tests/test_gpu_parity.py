@@ -227,6 +227,15 @@ def test_cls_prune_and_deferred_adds_are_bit_identical(gpu, dtype):
         d24 = rel(f24, groups["prune1"][0])
         print(f"[{cfg.name} {dtype}] 24-bit vs fp32 residual stream: rel {d24:.2e}")
         assert 0 < d24 < (1.5e-3 if dtype == "fp16" else 1e-2), (cfg.name, dtype, d24)
+        if "fold" in groups:  # the fold on the 24-bit stream (EPI_RES_STATS x24 planes)
+            eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning={"lnfold": 1})
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            g24 = eng.encode_image(px).clone()
+            eng.close()
+            e24 = rel(g24, groups["fold"][0])
+            print(f"[{cfg.name} {dtype}] folded: 24-bit vs fp32 residual stream: rel {e24:.2e}")
+            assert 0 < e24 < 1.5e-3, (cfg.name, dtype, e24)
 
 
 @pytest.mark.parametrize("dtype,pdt", [("fp16", torch.float16), ("bf16", torch.bfloat16)])
@@ -355,12 +364,13 @@ def test_config4_l14_336_bs128_as_benched(gpu):
     print(f"L/14@336 bs 128 (split + v80 tiles): max rel logit err {rel:.2e} on rows {idx}")
 
 
-def test_lnfold_bs256_runs_through_the_round_split(gpu):
+@pytest.mark.parametrize("x24", [1, 0])
+def test_lnfold_bs256_runs_through_the_round_split(gpu, x24):
     """the LayerNorm-fold path (tuning lnfold=1) at the headline batch, B/32 bs 256,
     where c_fc's 600 tiles take the whole-round row split. The ping-pong main tiles have only the
     16-bit STORE / GELU epilogues, so the folded c_fc (EPI_LNF_GELU) must take the single-launch
     path instead of failing. Rows from the start, middle and end of the batch against the oracle
-    at the 1e-3 bar (peaked text)."""
+    at the 1e-3 bar (peaked text), on the 24-bit residual stream and on fp32 x."""
     cfg = C.VIT_B32
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
@@ -368,7 +378,7 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu):
     px = _pixels(256, 224, seed=43)
     T = _text(cfg.embed_dim, 437, anchor=_anchor(ref_sd, cfg.name, 224))
     seg = [0, 40, 60, 359, 395, 425, 437]
-    eng = VisionEngine(cfg, 0, "fp16", max_batch=256, tuning={"lnfold": 1})
+    eng = VisionEngine(cfg, 0, "fp16", max_batch=256, tuning={"lnfold": 1, "x24": x24})
     try:
         eng.load_state_dict(sd)
         eng.load_lora(ad)
@@ -379,7 +389,7 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu):
         f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[idx])
         _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
         rel = _check_logits(o.logits[idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[("fp16", "peaked")])
-        print(f"B/32 bs 256 lnfold: max rel logit err {rel:.2e}")
+        print(f"B/32 bs 256 lnfold x24={x24}: max rel logit err {rel:.2e}")
     finally:
         eng.close()
 

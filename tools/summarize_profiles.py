@@ -1,6 +1,6 @@
 """Turn a tools/profile_round.sh output directory into committed summaries under profiles/.
 
-    python tools/summarize_profiles.py gpurun_out/prof r02 [images_per_launch]
+    python tools/summarize_profiles.py gpurun_out/prof r02 [images_per_launch] [--summary-only]
 writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim), profiles/<tag>_summary.md
 (per-kernel-role averages, MFMA TFLOP/s, PMC bytes per launch) and updates
 profiles/pmc_traffic.json (read by bench.py's roofline.traffic).
@@ -14,6 +14,8 @@ clipvit_profile_forward pass: one lane, serialised — what the bench's roofline
 "concurrent" otherwise (the timed loop's two lanes share the GPU).
 
 images_per_launch: images per GEMM launch (bs 256 with the default two-lane split: 128).
+--summary-only: write profiles/<tag>_summary.md only (A/B arms: no kernel_stats copy, no
+fc_traffic / pmc_traffic JSON).
 """
 import csv
 import json
@@ -129,12 +131,15 @@ def fc_split_rows(M, N=3072, ncu=256):
 
 
 def main():
-    src, tag = Path(sys.argv[1]), sys.argv[2]
-    lane_b = int(sys.argv[3]) if len(sys.argv) > 3 else 128
+    only = "--summary-only" in sys.argv
+    argv = [x for x in sys.argv if x != "--summary-only"]
+    src, tag = Path(argv[1]), argv[2]
+    lane_b = int(argv[3]) if len(argv) > 3 else 128
     prof = ROOT / "profiles"
     prof.mkdir(exist_ok=True)
     kt = next((src / "kt").rglob("*kernel_stats.csv"))
-    shutil.copyfile(kt, prof / f"{tag}_kernel_stats.csv")
+    if not only:
+        shutil.copyfile(kt, prof / f"{tag}_kernel_stats.csv")
     trace = load_rows(next((src / "kt").rglob("*kernel_trace.csv")))
     roles = roles_by_queue(trace)
     iso = isolated_flags(trace)
@@ -225,6 +230,8 @@ def main():
                      f"{(t['read_bytes'] + t['write_bytes']) / al:.2f} | {t['mfma_busy']:.3f} | {t['wait_share']:.3f} | "
                      f"{t['l2_hit']:.3f} |")
     (prof / f"{tag}_summary.md").write_text("\n".join(lines) + "\n")
+    if only:
+        return
     mlp = [traffic[r] for r in ("fc", "proj") if r in traffic]
     entry = {"mlp_gemm_bytes_per_launch": sum(t["read_bytes"] + t["write_bytes"] for t in mlp) / len(mlp),
              "mlp_gemm_avg_us": sum(t["avg_us"] for t in mlp) / len(mlp), "source": f"profiles/{tag}_summary.md",
