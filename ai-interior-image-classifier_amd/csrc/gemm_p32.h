@@ -65,8 +65,10 @@ __device__ void p32_store16(u32x4 vdata, i32x4_t rsrc, int voffset, int soffset,
 // panel, so that operand is an L2 hit after its first fetch
 // ABL (diagnostic, outputs garbage): 7 = no staging after the prologue, 8 = no MFMA, 9 = no
 // fragment reads, 3 = no epilogue stores, 4 = row-major stores into rows m & 255 only
+// AGP: accumulators in AGPRs (inline-asm MFMAs, "+a"; the bias added in the epilogue instead of
+// being the first MFMA's C), so the MFMAs' C / D traffic leaves the VGPR file to the fragment reads
 template <typename T, int EPI, bool BLKA, bool BLKW, int STP, int GRP, class HK, bool ROT = false, int RES = 0,
-          bool RD1 = false, int ABL = 0>
+          bool RD1 = false, int ABL = 0, bool AGP = false>
 __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -157,7 +159,10 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                  : "=v"(a_hi), "=v"(w_hi)
                  : "v"(a_lo), "v"(w_lo));
     auto rd = [&](vec8& d, unsigned base, auto imm) {
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
+        if constexpr (AGP)  // (AGP: the fragments live in AGPRs too, the MFMAs read them there)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=a"(d) : "v"(base), "i"(decltype(imm)::value));
+        else
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
     };
     auto reads = [&](auto stc) {
         constexpr int ST = decltype(stc)::value, SO = (ST & 1) * STAGE;
@@ -183,8 +188,23 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         for (int fm = 0; fm < 8; ++fm)
 #pragma unroll
             for (int fn = 0; fn < 4; ++fn) {
-                if constexpr (ABL == 8) asm volatile("" ::"v"(wf[fn]), "v"(af[fm]));
-                else acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                if constexpr (ABL == 8) {
+                    asm volatile("" ::"v"(wf[fn]), "v"(af[fm]));
+                } else if constexpr (AGP) {
+                    if constexpr (FIRST) {
+                        if constexpr (std::is_same<T, F16>::value)
+                            asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                        else
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                    } else {
+                        if constexpr (std::is_same<T, F16>::value)
+                            asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                        else
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                    }
+                } else {
+                    acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                }
             }
         __builtin_amdgcn_s_setprio(0);
     };
@@ -213,6 +233,12 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         int le;
         asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
         const int n = pn0 + wc * 64 + 16 * (le >> 4);
+        if constexpr (AGP) {
+            // the last MFMAs' AGPR results -> the v_accvgpr_reads below: 16 wait states (>= the 12
+            // an 8-pass XDL result needs), then this tile's bias slice
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            load_bias(pn0);
+        }
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
@@ -220,7 +246,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = AGP ? acc[f][fm][rr] + bv[f][rr] : acc[f][fm][rr];
             if constexpr (GELU) {
 #pragma unroll
                 for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
@@ -309,7 +335,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             else null_stores();
             hk.mark(ti, 1);
         }
-        if constexpr (decltype(first)::value) load_bias(n0);
+        if constexpr (decltype(first)::value && !AGP) load_bias(n0);
         if constexpr (!RF) reads(stc);
         if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
         bar(step, 0);
@@ -388,15 +414,15 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 }
 
 template <typename T, int EPI, bool BLKA, bool BLKW = false, int STP = 0, class HK = P32Barrier, bool ROT = false,
-          int RES = 0, bool RD1 = false, int ABL = 0>
+          int RES = 0, bool RD1 = false, int ABL = 0, bool AGP = false>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     HK hk;
     hk.init(smem, lane, wave);
-    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, STP, 0, HK, ROT, RES, RD1, ABL>(a, ntiles, smem, lane, wave, hk);
-    else p32_body<T, EPI, BLKA, BLKW, STP, 1, HK, ROT, RES, RD1, ABL>(a, ntiles, smem, lane, wave - 4, hk);
+    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, STP, 0, HK, ROT, RES, RD1, ABL, AGP>(a, ntiles, smem, lane, wave, hk);
+    else p32_body<T, EPI, BLKA, BLKW, STP, 1, HK, ROT, RES, RD1, ABL, AGP>(a, ntiles, smem, lane, wave - 4, hk);
     hk.done(a);
 }
 

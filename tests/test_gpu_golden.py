@@ -42,7 +42,12 @@ from interior_amd.weights import synthetic_text_state_dict
 
 pytestmark = pytest.mark.gpu
 LOGIT_TOL = 1e-3
-FLAT_TOL = 3e-3  # flat fixtures: twice the committed worst image (1.42e-3, r03), not the bar
+# flat fixtures: the worst image per case is a TRACKED number (README; r05 run of this
+# test: B/32 1.28e-3 / 1.42e-3, B/16 6.34e-4 / 5.95e-4). B/16 is held to the 1e-3 bar itself; B/32,
+# whose flat rows inflate the relative measure (module docstring), to its tracked worst + 10 %
+FLAT_WORST = {("vitb32", "lora"): 1.28e-3, ("vitb32", "lora_new"): 1.42e-3,
+              ("vitb16", "lora"): 6.34e-4, ("vitb16", "lora_new"): 5.95e-4}
+FLAT_TOL = max(FLAT_WORST.values()) * 1.1  # the bound for the swap rule's error cap
 GAP_TOL = 1e-4   # fixture probability gap below which two labels may swap
 PROB_TOL = 2e-3
 TEXT_TOL = 2e-3
@@ -157,9 +162,10 @@ def test_flat_fixtures_results_match_reference_harness(gpu, golden_dir, images, 
         print(f"\n[{model}/{ckpt}] rel logit err over {len(rel)} images: worst {worst:.2e} "
               f"({names[int(rel.argmax())]}), p95 {np.percentile(rel, 95):.2e}, median {np.median(rel):.2e}, "
               f"> 1e-3: {int((rel > 1e-3).sum())}")
-        # flat logits inflate this relative measure (module docstring): the 1e-3 bar is asserted on
-        # the CLIP-scale fixtures; here a loose bound of twice the committed worst (1.42e-3, r03)
-        assert worst <= FLAT_TOL, (model, ckpt, worst, names[int(rel.argmax())])
+        # flat logits inflate this relative measure (module docstring): the 1e-3 bar where the
+        # tracked worst is below it (B/16), else the tracked worst + 10 % (B/32)
+        bound = max(LOGIT_TOL, 1.1 * FLAT_WORST[(model, ckpt)])
+        assert worst <= bound, (model, ckpt, worst, bound, names[int(rel.argmax())])
         # per-segment argmax: identical unless the reference's top-1/top-2 margin is within
         # twice this image's absolute logit error
         off, exempt, checked = an.table.offsets, 0, 0

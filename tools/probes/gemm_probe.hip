@@ -785,6 +785,14 @@ int main(int argc, char** argv) {
                 run("p32 blocked: no fragment reads", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 9><<<grid, 512>>>(a, ntiles); });
                 run("p32 blocked: no stores", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 3><<<grid, 512>>>(a, ntiles); });
             }
+            run("p32 W blocked, AGPR accumulators", [&] {
+                if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
+                else gemm_p32_kernel<F16, EPI_STORE, false, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
+            });
+            run("p32 A + W blocked, AGPR accumulators", [&] {
+                if (epi) gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
+                else gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
+            });
             run("p32 W blocked: stores into 256 rows", [&] {
                 if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, 0, P32Barrier, false, 0, false, 4><<<grid, 512>>>(a, ntiles);
                 else gemm_p32_kernel<F16, EPI_STORE, false, true, 0, P32Barrier, false, 0, false, 4><<<grid, 512>>>(a, ntiles);
