@@ -1,7 +1,9 @@
 // Persistent 256x256 MFMA GEMM with 32-deep k-steps and a four-stage LDS ring (variant 72;
-// round 5). Included by gemm_pp.hip. tools/probes/gemm_p32_diag.h is a copy of this kernel with the
-// diagnostic hooks of profiles/r05_gemm_timeline.md (per-barrier s_memtime stamps, ablations,
-// store policies, AGPR accumulators) for tools/probes/gemm_probe.hip; keep the two in step.
+// round 5): DIAGNOSTIC COPY of ai-interior-image-classifier_amd/csrc/gemm_p32.h for
+// tools/probes/gemm_probe.hip only (never built into the library). Same instruction stream at the
+// default template arguments, plus the hooks of profiles/r05_gemm_timeline.md: a barrier policy
+// that stamps s_memtime, store cache policies (STP), k-rotation (ROT), L2-resident operands
+// (RES), read order (RD1), ablations (ABL) and AGPR accumulators (AGP).
 //
 //   C[M, N] = A[M, K] @ W[N, K]^T + bias   (16-bit C; QuickGELU for c_fc)
 //
@@ -45,8 +47,33 @@
 
 namespace clipvit {
 
-template <typename T, int EPI, bool BLKA, bool BLKW, int GRP>
-__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc) {
+// Barrier policy of the kernel: the library's is the plain s_barrier. tools/probes/gemm_probe.hip
+// instantiates the kernel with a policy that also stamps s_memtime around every barrier (the
+// timeline of profiles/r05_gemm_timeline.md); the instruction stream between barriers is the same.
+struct P32Barrier {
+    __device__ __forceinline__ void bar(int /*tile*/, int /*step*/, int /*seg*/) { __builtin_amdgcn_s_barrier(); }
+    __device__ __forceinline__ void mark(int /*tile*/, int /*which*/) {}
+    __device__ __forceinline__ void sub(int /*tile*/, int /*step*/) {}
+    __device__ __forceinline__ void init(unsigned char*, int, int) {}
+    __device__ __forceinline__ void done(const GemmArgs&) {}
+};
+
+__device__ void p32_store16(u32x4 vdata, i32x4_t rsrc, int voffset, int soffset, int aux) __asm(
+    "llvm.amdgcn.raw.buffer.store.v4i32");
+
+// STP: cache policy of the epilogue stores (0 = plain global stores; else the aux bits of a
+// buffer store: 16 = sc1, which writes through without keeping the line in the XCD's L2, 2 = nt)
+// ROT: each tile walks its k-steps from (nt & 3) * nk / 4 on, wrapping (diagnostic: CUs that
+// share an operand panel then request different k-slices at a given time)
+// RES (diagnostic, outputs garbage): 1 = every tile stages the first W panel, 2 = the first A
+// panel, so that operand is an L2 hit after its first fetch
+// ABL (diagnostic, outputs garbage): 7 = no staging after the prologue, 8 = no MFMA, 9 = no
+// fragment reads, 3 = no epilogue stores, 4 = row-major stores into rows m & 255 only
+// AGP: accumulators in AGPRs (inline-asm MFMAs, "+a"; the bias added in the epilogue instead of
+// being the first MFMA's C), so the MFMAs' C / D traffic leaves the VGPR file to the fragment reads
+template <typename T, int EPI, bool BLKA, bool BLKW, int STP, int GRP, class HK, bool ROT = false, int RES = 0,
+          bool RD1 = false, int ABL = 0, bool AGP = false>
+__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
     constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 KB + 16 KB
@@ -73,7 +100,9 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     const unsigned char* const src = (const unsigned char*)(GRP == 0 ? a.A : a.W);
     const int rows = GRP == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;  // (N % 256 == 0)
     auto rsrc_of = [&](int m0, int n0) {
-        const int r0 = GRP == 0 ? m0 : n0;
+        int r0 = GRP == 0 ? m0 : n0;
+        if constexpr (RES == 1) { if (GRP == 1) r0 = 0; }
+        if constexpr (RES == 2) { if (GRP == 0) r0 = 0; }
         const size_t bytes = (size_t)(rows - r0) * ldb;
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
     };
@@ -94,9 +123,15 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     auto koff = [&](int kk) { return OWN_BLK ? (kk >> 1) * 2048 + (kk & 1) * 1024 : kk * 64; };
     using T_ = std::true_type;
     using F_ = std::false_type;
-    auto stage_pieces = [&](const i32x4_t& r, int kk, int st) {
+    int rot_c = 0, rot_n = 0;  // (ROT) k-step rotation of the current / next tile
+    auto stage_pieces = [&](const i32x4_t& r, int kk, int st, int rot) {
         unsigned char* dst = smem + st * STAGE + opbase + 4 * wc * 1024;
+        if constexpr (ROT) {
+            kk += rot;
+            if (kk >= nk) kk -= nk;
+        }
         const int so = koff(kk);
+        if constexpr (ABL == 7) return;
 #pragma unroll
         for (int i = 0; i < 4; ++i) blds16(r, voff[i], so, dst + i * 1024);
     };
@@ -128,10 +163,14 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                  : "=v"(a_hi), "=v"(w_hi)
                  : "v"(a_lo), "v"(w_lo));
     auto rd = [&](vec8& d, unsigned base, auto imm) {
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
+        if constexpr (AGP)  // (AGP: the fragments live in AGPRs too, the MFMAs read them there)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=a"(d) : "v"(base), "i"(decltype(imm)::value));
+        else
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
     };
     auto reads = [&](auto stc) {
         constexpr int ST = decltype(stc)::value, SO = (ST & 1) * STAGE;
+        if constexpr (ABL == 9) return;
         const unsigned ba = ST >= 2 ? a_hi : a_lo, bw = ST >= 2 ? w_hi : w_lo;
         rd(wf[0], bw, std::integral_constant<int, SO>{});
         rd(wf[1], bw, std::integral_constant<int, SO + 1024>{});
@@ -153,13 +192,30 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         for (int fm = 0; fm < 8; ++fm)
 #pragma unroll
             for (int fn = 0; fn < 4; ++fn) {
-                acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                if constexpr (ABL == 8) {
+                    asm volatile("" ::"v"(wf[fn]), "v"(af[fm]));
+                } else if constexpr (AGP) {
+                    if constexpr (FIRST) {
+                        if constexpr (std::is_same<T, F16>::value)
+                            asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0" : "=a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                        else
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                    } else {
+                        if constexpr (std::is_same<T, F16>::value)
+                            asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                        else
+                            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
+                    }
+                } else {
+                    acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                }
             }
         __builtin_amdgcn_s_setprio(0);
     };
-    auto bar = [&] {
+    int ti = 0;  // tiles done by this workgroup (barrier policy only)
+    auto bar = [&](int step, int seg) {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        hk.bar(ti, step, seg);
         __builtin_amdgcn_sched_barrier(0);
     };
     // the tile's bias vector slice (16 features per lane) from LDS: inline asm with its own wait
@@ -174,12 +230,19 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             : "memory");
     };
     unsigned char* const Cb = (unsigned char*)a.C;
+    const i32x4_t rs_out = buf_rsrc(a.C, 0xFFFFFFFFu);  // (STP != 0) C < 4 GB
     auto epilogue = [&](int pm0, int pn0) {
         // lane-derived addresses recomputed here from an opaque copy of the lane id: hipcc
         // otherwise hoists the per-row offsets of all 16 stores out of the tile loop and spills
         int le;
         asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
         const int n = pn0 + wc * 64 + 16 * (le >> 4);
+        if constexpr (AGP) {
+            // the last MFMAs' AGPR results -> the v_accvgpr_reads below: 16 wait states (>= the 12
+            // an 8-pass XDL result needs), then this tile's bias slice
+            asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+            load_bias(pn0);
+        }
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
@@ -187,7 +250,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = AGP ? acc[f][fm][rr] + bv[f][rr] : acc[f][fm][rr];
             if constexpr (GELU) {
 #pragma unroll
                 for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
@@ -213,12 +276,18 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                     w1[d] = r[1];
                 }
                 const int g = le >> 4;
-                off = ((size_t)m * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
+                const int ms = ABL == 4 ? (m & 255) : m;  // (ABL 4: every tile's rows alias one L2-resident band)
+                off = ((size_t)ms * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
                 off2 = off + 64;
             }
-            if (m < a.M) {
-                *(u32x4*)(Cb + off) = w0;
-                *(u32x4*)(Cb + off2) = w1;
+            if (m < a.M && (ABL != 3 || a.ldc < 0)) {
+                if constexpr (STP == 0) {
+                    *(u32x4*)(Cb + off) = w0;
+                    *(u32x4*)(Cb + off2) = w1;
+                } else {
+                    p32_store16(w0, rs_out, (int)off, 0, STP);
+                    p32_store16(w1, rs_out, (int)off2, 0, STP);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
         }
@@ -256,18 +325,24 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         // ---- read segment: staging issue first (it does not wait for anything), then group 1's
         // counted wait, the previous tile's epilogue (its stores younger than every piece the
         // next waits count), the tile's bias slice, the fragment reads ----
-        stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value);
+        constexpr bool RF = RD1 && !EP && !decltype(first)::value;  // fragment reads before the staging
+        if constexpr (RF) reads(stc);
+        stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value,
+                     decltype(nxt)::value ? rot_n : rot_c);
+        hk.sub(ti, step);
         if constexpr (GRP == 1) {  // pieces of step t + 1 (issued two read segments ago) landed
             if (W24) vm_wait<24>(); else vm_wait<8>();
         }
         if constexpr (EP) {
+            hk.mark(ti, 0);
             if (have_prev) epilogue(pm0, pn0);
             else null_stores();
+            hk.mark(ti, 1);
         }
-        if constexpr (decltype(first)::value) load_bias(n0);
-        reads(stc);
+        if constexpr (decltype(first)::value && !AGP) load_bias(n0);
+        if constexpr (!RF) reads(stc);
         if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
-        bar();
+        bar(step, 0);
         // ---- MFMA segment ----
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the fragment reads (inline asm) landed
         __builtin_amdgcn_sched_barrier(0);
@@ -276,12 +351,15 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         if constexpr (GRP == 0) {
             if (W24) vm_wait<24>(); else vm_wait<8>();
         }
-        bar();
+        bar(step, 1);
     };
     // prologue: steps 0, 1, 2 of the first tile; the bias vector of the whole GEMM -> LDS
-    stage_pieces(rs_c, 0, 0);
-    stage_pieces(rs_c, 1, 1);
-    stage_pieces(rs_c, 2, 2);
+    auto rot_of = [&](int n0) { return ROT ? ((n0 / BN) & 3) * (nk >> 2) : 0; };
+    rot_c = rot_of(n0);
+    rot_n = rot_of(nn);
+    stage_pieces(rs_c, 0, 0, rot_c);
+    stage_pieces(rs_c, 1, 1, rot_c);
+    stage_pieces(rs_c, 2, 2, rot_c);
     {
         float* cv = (float*)(smem + 4 * STAGE);
         for (int i = (GRP * 256 + wc * 64 + lane); i < a.N; i += 512) cv[i] = a.bias ? a.bias[i] : 0.f;
@@ -320,27 +398,36 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         kstep(nk - 3, 0, T_{}, S1{}, S0{}, F_{}, F_{}, F_{}, false, 0, 0);
         kstep(nk - 2, 1, T_{}, S2{}, S1{}, F_{}, F_{}, F_{}, false, 0, 0);
         kstep(nk - 1, 2, T_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
+        ++ti;
         pm0 = m0;
         pn0 = n0;
         if (!has_next) break;
         m0 = mn;
         n0 = nn;
         rs_c = rs_n;
+        rot_c = rot_n;
         has_next = tile(i + 1, mn, nn);
+        rot_n = rot_of(nn);
         rs_n = has_next ? rsrc_of(mn, nn) : rs_none;
     }
+    hk.mark(ti, 0);
     epilogue(pm0, pn0);
+    hk.mark(ti, 1);
     if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
     vm_wait<0>();
 }
 
-template <typename T, int EPI, bool BLKA, bool BLKW = false>
+template <typename T, int EPI, bool BLKA, bool BLKW = false, int STP = 0, class HK = P32Barrier, bool ROT = false,
+          int RES = 0, bool RD1 = false, int ABL = 0, bool AGP = false>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, 0>(a, ntiles, smem, lane, wave);
-    else p32_body<T, EPI, BLKA, BLKW, 1>(a, ntiles, smem, lane, wave - 4);
+    HK hk;
+    hk.init(smem, lane, wave);
+    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, STP, 0, HK, ROT, RES, RD1, ABL, AGP>(a, ntiles, smem, lane, wave, hk);
+    else p32_body<T, EPI, BLKA, BLKW, STP, 1, HK, ROT, RES, RD1, ABL, AGP>(a, ntiles, smem, lane, wave - 4, hk);
+    hk.done(a);
 }
 
 }  // namespace clipvit

@@ -19,7 +19,7 @@
 #include <vector>
 
 #include "../../ai-interior-image-classifier_amd/csrc/common.h"
-#include "../../ai-interior-image-classifier_amd/csrc/gemm_p32.h"
+#include "gemm_p32_diag.h"
 
 using namespace clipvit;
 
