@@ -163,8 +163,11 @@ struct clipvit_handle {
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
     // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
     // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
-    // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). tuning large_variants="q,f,o,p"
-    int large_var[4] = {3462, 3463, 3463, 3463};  // QKV, c_fc, out_proj, c_proj
+    // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). r05: the 32-deep-k-step tile (3472, gemm_p32.h)
+    // on every role with QKV / c_fc reading their blocked weight copies (w_blk): L/14@336 bs 128
+    // 2,406 / 2,407 -> 2,526 / 2,529 img/s (same box, profiles/r05/l14_ab.txt).
+    // tuning large_variants="q,f,o,p"
+    int large_var[4] = {3472, 3472, 3472, 3472};  // QKV, c_fc, out_proj, c_proj
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (tuning gemm_xcd="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -254,7 +257,10 @@ struct clipvit_handle {
     // accumulator-layout stores become 256-B runs per quarter-wave instead of 16 scattered
     // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
     bool u_blk = true;
-    bool w_blk = false;  // tuning w_blocked: QKV / c_fc weights also in the 16-row blocked layout
+    // QKV / c_fc weights also in the 16-row blocked layout (GemmArgs.blk_w), read by: 1 = the
+    // launches on the 32-deep-k-step tile (72: the large-M roles), 2 = every launch whose tile
+    // reads it (B/32 measured neutral to -0.7 %), 0 = none (no copies). tuning w_blocked
+    int w_blk = 1;
 };
 
 static std::string L(int i, const char* leaf) {
@@ -432,7 +438,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     int variant = h->var[role];
     // the blocked copy of W (w_blocked) for the launches whose tile reads it
     auto wsel = [&](GemmArgs& g, int v) {
-        const bool blk = Wb && h->w_blk && v >= 8 && v != 62 && v != 63 && g.ksplit <= 1;
+        const bool blk = Wb && g.ksplit <= 1 &&
+                         (h->w_blk == 2 ? (v >= 8 && v != 62 && v != 63) : (h->w_blk == 1 && v == 72));
         g.W = blk ? Wb : W;
         g.blk_w = blk;
     };
@@ -1037,6 +1044,14 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
     h->lnfold = false;
     h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);
+    // large-M roles at width 768 (B/16): the 32-deep-k-step tile wins only on c_fc there; QKV
+    // and out_proj / c_proj keep the r04 ping-pong tiles (same box, B/16 bs 256: QKV 1.17 -> 1.30
+    // ms per forward on 3472, c_fc 1.42 -> 1.33; profiles/r05/large_ab.txt)
+    if (c.width <= 768) {
+        h->large_var[0] = 3462;
+        h->large_var[2] = 3463;
+        h->large_var[3] = 3463;
+    }
     // default bf16 blocks: the MLP of the first two and last two blocks, the attention roles of
     // block 1 and the last block only (the last block runs the class-token tail). Measured on
     // three image / text seeds against the bf16 engine at CLIP logit scale: 1.79e-2 (bar 2e-2;
@@ -1110,7 +1125,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
-    else if (k == "w_blocked") ok = flag(h->w_blk);
+    else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72)
         int m[2] = {h->split_main, h->split_tail};
         ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72);
@@ -1169,8 +1184,8 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, w_blk;
-        int split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk;
+        int w_blk, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
@@ -1255,7 +1270,7 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
-    const bool wblk = h->w_blk && !h->mx8;  // blocked QKV / c_fc weight copies
+    const bool wblk = h->w_blk != 0 && !h->mx8;  // blocked QKV / c_fc weight copies
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         HIPCHK(alloc16(ly.wqkv, 3 * D * D));

@@ -429,22 +429,25 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
 
 
 @pytest.mark.parametrize("name,dtype,B,tun", [
-    ("ViT-B/32", "fp16", 256, {}),                            # QKV v98, c_fc tail v81 read the copy
+    ("ViT-B/32", "fp16", 256, {}),                            # QKV v98, c_fc tail v81 read the copy (2)
     ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),   # 32-deep-k-step c_fc main
     ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}),          # one launch per role, ragged M
     ("ViT-B/16", "fp16", 64, {}),                             # N = 197, round split
+    ("ViT-B/16", "fp16", 256, {}),                            # large M: every role on 3472 (default)
+    ("ViT-L/14@336px", "fp16", 32, {}),                       # large M, the shipped 3472 roles
     ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}),  # large-M pipelined tiles
 ])
 def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun):
-    """QKV / c_fc weights read from their 16-row blocked copy (tuning w_blocked=1) move bytes
-    only: every tile computes the same products in the same order, so the features equal the
-    row-major run's bit for bit — after a LoRA merge, which re-packs both copies."""
+    """QKV / c_fc weights read from their 16-row blocked copy (tuning w_blocked: 1 = the
+    variant-72 launches, the default; 2 = every tile that can) move bytes only: every tile
+    computes the same products in the same order, so the features equal the row-major run's
+    (w_blocked=0) bit for bit — after a LoRA merge, which re-packs both copies."""
     cfg = C.get_config(name)
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
     px = _pixels(B, cfg.image_size, seed=53).to(gpu)
     outs = []
-    for blk in (1, 0):
+    for blk in (2, 1, 0):
         eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk))
         try:
             eng.load_state_dict(sd)
@@ -454,4 +457,4 @@ def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun):
         finally:
             eng.close()
     assert torch.isfinite(outs[0]).all()
-    assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2]), (name, dtype, B, tun)
