@@ -165,9 +165,11 @@ struct clipvit_handle {
     // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
     // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). r05: the 32-deep-k-step tile (3472, gemm_p32.h)
     // on every role with QKV / c_fc reading their blocked weight copies (w_blk): L/14@336 bs 128
-    // 2,406 / 2,407 -> 2,526 / 2,529 img/s (same box, profiles/r05/l14_ab.txt).
+    // 2,406 / 2,407 -> 2,526 / 2,529 img/s (same box, profiles/r05/l14_ab.txt); c_fc with
+    // non-temporal stores (3474: its u no longer sits dirty in front of the next QKV): L/14
+    // 2,522 / 2,586 -> 2,614 / 2,613, B/16 24.1k / 24.2k -> 24.5k / 24.5k (profiles/r05/nt_*).
     // tuning large_variants="q,f,o,p"
-    int large_var[4] = {3472, 3472, 3472, 3472};  // QKV, c_fc, out_proj, c_proj
+    int large_var[4] = {3472, 3474, 3472, 3472};  // QKV, c_fc, out_proj, c_proj
     int ncu = 256;            // compute units of the device
     // tile->XCD partition per role (tuning gemm_xcd="q,o,f,p,e"): 2 = 4x2 (M, N) XCD grid,
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
@@ -439,7 +441,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the blocked copy of W (w_blocked) for the launches whose tile reads it
     auto wsel = [&](GemmArgs& g, int v) {
         const bool blk = Wb && g.ksplit <= 1 &&
-                         (h->w_blk == 2 ? (v >= 8 && v != 62 && v != 63) : (h->w_blk == 1 && v == 72));
+                         (h->w_blk == 2 ? (v >= 8 && v != 62 && v != 63) : (h->w_blk == 1 && (v == 72 || v == 74)));
         g.W = blk ? Wb : W;
         g.blk_w = blk;
     };
@@ -1044,9 +1046,9 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
     h->lnfold = false;
     h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);
-    // large-M roles at width 768 (B/16): the 32-deep-k-step tile wins only on c_fc there; QKV
-    // and out_proj / c_proj keep the r04 ping-pong tiles (same box, B/16 bs 256: QKV 1.17 -> 1.30
-    // ms per forward on 3472, c_fc 1.42 -> 1.33; profiles/r05/large_ab.txt)
+    // large-M roles at width 768 (B/16): the 32-deep-k-step tile wins only on c_fc there (1.42 ->
+    // 1.31 ms per forward on 3474); QKV and out_proj / c_proj keep the r04 ping-pong tiles
+    // (profiles/r05/large_ab.txt, b16_ab3.txt, nt_b16_ab.txt)
     if (c.width <= 768) {
         h->large_var[0] = 3462;
         h->large_var[2] = 3463;
@@ -1126,9 +1128,9 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
-    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72)
+    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72);
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72 || m[0] == 74);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
@@ -1594,7 +1596,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 72;
+                        variant == 63 || variant == 72 || variant == 74;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

@@ -45,7 +45,9 @@
 
 namespace clipvit {
 
-template <typename T, int EPI, bool BLKA, bool BLKW, int GRP>
+// NT: non-temporal epilogue stores (variant 74: the large-M c_fc, whose u would otherwise sit
+// dirty in the L2 / Infinity Cache in front of the next blocks' operands)
+template <typename T, int EPI, bool BLKA, bool BLKW, int GRP, bool NT>
 __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -217,8 +219,13 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                 off2 = off + 64;
             }
             if (m < a.M) {
-                *(u32x4*)(Cb + off) = w0;
-                *(u32x4*)(Cb + off2) = w1;
+                if constexpr (NT) {
+                    __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
+                    __builtin_nontemporal_store(w1, (u32x4*)(Cb + off2));
+                } else {
+                    *(u32x4*)(Cb + off) = w0;
+                    *(u32x4*)(Cb + off2) = w1;
+                }
             }
             __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
         }
@@ -334,13 +341,13 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     vm_wait<0>();
 }
 
-template <typename T, int EPI, bool BLKA, bool BLKW = false>
+template <typename T, int EPI, bool BLKA, bool BLKW = false, bool NT = false>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, 0>(a, ntiles, smem, lane, wave);
-    else p32_body<T, EPI, BLKA, BLKW, 1>(a, ntiles, smem, lane, wave - 4);
+    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, 0, NT>(a, ntiles, smem, lane, wave);
+    else p32_body<T, EPI, BLKA, BLKW, 1, NT>(a, ntiles, smem, lane, wave - 4);
 }
 
 }  // namespace clipvit
