@@ -61,8 +61,8 @@ struct DeviceGuard {
 
 struct LayerW {
     void *wqkv = nullptr, *wout = nullptr, *wfc = nullptr, *wproj = nullptr;
-    // QKV / c_fc weights again in the 16-row blocked layout (GemmArgs.blk_w), with w_blocked
-    void *wqkv_b = nullptr, *wfc_b = nullptr;
+    // the Linear weights again in the 16-row blocked layout (GemmArgs.blk_w), with w_blocked
+    void *wqkv_b = nullptr, *wfc_b = nullptr, *wout_b = nullptr, *wproj_b = nullptr;
     const float *bqkv, *bout, *bfc, *bproj, *ln1g, *ln1b, *ln2g, *ln2b;
     // LayerNorm fold (lnfold): ln_1 into QKV, ln_2 into c_fc: s_n = sum_k W'_nk, b' = b + W beta
     float *s_qkv = nullptr, *bf_qkv = nullptr, *s_fc = nullptr, *bf_fc = nullptr;
@@ -705,7 +705,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         const int eo = r16 ? EPI_STORE : EPI_RESID;
         void* co = r16 ? y : (void*)w->x;
         rc = q ? gemm8(s, h, eo, q8, ly.wout, ly.bout, co, M, D, D, D, R_OUT)
-               : gemm(s, h, eo, w->h, ly.wout, ly.bout, co, M, D, D, D, R_OUT);
+               : gemm(s, h, eo, w->h, ly.wout, ly.bout, co, M, D, D, D, R_OUT, Fold(), w, ly.wout_b);
         if (rc) return rc;
         if (prof) prof->mark(s, F_OUT);
         if (r16) add_ln(y, nullptr, ly.ln2g, ly.ln2b, qm, defer);
@@ -722,7 +722,7 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         const int ep = p16 ? EPI_STORE : EPI_RESID;
         void* cp = p16 ? (defer ? y2 : y) : (void*)w->x;
         rc = qm ? gemm8(s, h, ep, u8, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ, ublk)
-               : gemm(s, h, ep, w->u, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ);
+               : gemm(s, h, ep, w->u, ly.wproj, ly.bproj, cp, M, D, 4 * D, D, R_PROJ, Fold(), w, ly.wproj_b);
         if (rc) return rc;
         if (prof) prof->mark(s, F_PROJ);
         if (!last) {
@@ -874,7 +874,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         }
         const bool defer = h->resid16 && h->defer_x && !last;
         if (h->resid16) {
-            if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT))) return rc;
+            if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT, Fold(), w, ly.wout_b))) return rc;
             if (prof) prof->mark(s, F_OUT);
             if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D, X24, X24 != nullptr);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
@@ -889,7 +889,8 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
             void* yo = defer ? y2 : y;
-            if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, yo, M, D, 4 * D, D, R_PROJ))) return rc;
+            if ((rc = gemm(s, h, EPI_STORE, w->u, ly.wproj, ly.bproj, yo, M, D, 4 * D, D, R_PROJ, Fold(), w, ly.wproj_b)))
+                return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
             if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr);
@@ -996,7 +997,8 @@ static int pack_linear(clipvit_handle* h, hipStream_t s, const std::string& name
     launch_pack_weight(s, h->dt, w, dst, N, K, Kp);
     if (layer >= 0) {  // the blocked copy (w_blocked) follows every re-pack (LoRA merges too)
         const LayerW& ly = h->layers[layer];
-        void* blk = dst == ly.wqkv ? ly.wqkv_b : dst == ly.wfc ? ly.wfc_b : nullptr;
+        void* blk = dst == ly.wqkv ? ly.wqkv_b : dst == ly.wfc ? ly.wfc_b : dst == ly.wout ? ly.wout_b
+                  : dst == ly.wproj ? ly.wproj_b : nullptr;
         if (blk) launch_blk16_relayout(s, dst, blk, N, Kp);
     }
     return 0;
@@ -1272,7 +1274,7 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
-    const bool wblk = h->w_blk != 0 && !h->mx8;  // blocked QKV / c_fc weight copies
+    const bool wblk = h->w_blk != 0 && !h->mx8;  // blocked weight copies of the four Linears
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         HIPCHK(alloc16(ly.wqkv, 3 * D * D));
@@ -1282,6 +1284,8 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
         if (wblk) {
             HIPCHK(alloc16(ly.wqkv_b, 3 * D * D));
             HIPCHK(alloc16(ly.wfc_b, 4 * D * D));
+            HIPCHK(alloc16(ly.wout_b, D * D));
+            HIPCHK(alloc16(ly.wproj_b, 4 * D * D));
         }
         ly.bqkv = h->master[L(i, "attn.in_proj_bias")];
         ly.bout = h->master[L(i, "attn.out_proj.bias")];
@@ -1540,6 +1544,8 @@ int clipvit_destroy(clipvit_handle* h) {
         hipFree(ly.wfc);
         hipFree(ly.wqkv_b);
         hipFree(ly.wfc_b);
+        hipFree(ly.wout_b);
+        hipFree(ly.wproj_b);
         hipFree(ly.wproj);
     }
     hipFree(h->scratch);

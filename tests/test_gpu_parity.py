@@ -434,7 +434,8 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
     ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}),          # one launch per role, ragged M
     ("ViT-B/16", "fp16", 64, {}),                             # N = 197, round split
     ("ViT-B/16", "fp16", 256, {}),                            # large M: every role on 3472 (default)
-    ("ViT-L/14@336px", "fp16", 32, {}),                       # large M, the shipped 3472 roles
+    ("ViT-L/14@336px", "fp16", 32, {}),                       # large M: c_fc on the shipped 3474
+    ("ViT-L/14@336px", "fp16", 64, {}),                       # every role large-M: 3472 / 3474, blocked A
     ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}),  # large-M pipelined tiles
 ])
 def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun):
