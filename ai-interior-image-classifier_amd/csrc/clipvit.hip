@@ -1048,14 +1048,6 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
     h->lnfold = false;
     h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);
-    // large-M roles at width 768 (B/16): the 32-deep-k-step tile wins only on c_fc there (1.42 ->
-    // 1.31 ms per forward on 3474); QKV and out_proj / c_proj keep the r04 ping-pong tiles
-    // (profiles/r05/large_ab.txt, b16_ab3.txt, nt_b16_ab.txt)
-    if (c.width <= 768) {
-        h->large_var[0] = 3462;
-        h->large_var[2] = 3463;
-        h->large_var[3] = 3463;
-    }
     // default bf16 blocks: the MLP of the first two and last two blocks, the attention roles of
     // block 1 and the last block only (the last block runs the class-token tail). Measured on
     // three image / text seeds against the bf16 engine at CLIP logit scale: 1.79e-2 (bar 2e-2;
