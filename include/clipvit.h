@@ -97,8 +97,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * alternatives DESIGN.md records instead of the shipped default, before clipvit_load_weights
  * (CLIPVIT_E_STATE after it). spec = "key=value;key=value", keys: resid16, defer_x, lnfold,
  * cls_prune, round_split, attn_q8, x16, x24, u_blocked (0/1); w_blocked (0/1/2: the Linear
- * weights also kept in the 16-row blocked layout, read by the variant-72 / 74 launches (1,
- * default) or by every tile that can (2); 0 = no copies);
+ * weights also kept in the 16-row blocked layout, read by every tile that can (2, default) or
+ * by the variant-72 / 74 launches only (1); 0 = no copies);
  * split_variants "main,tail"; tail_variant; tail_kmin (>= 64, multiple of 64) / tail_smax (1..48):
  * the class-token tail's split-K rule; head_cols (64 / 32); mx8_split_tail (0, 2, 5);
  * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
