@@ -19,10 +19,11 @@
 //    stages W), and the tile-boundary crossing of the k-step stream is unrolled: the k-loop has
 //    no run-time branches; a missing next tile is a zero-length buffer resource (its pieces
 //    read as zeros into a stage nobody reads);
-//  * the bias is the accumulators' initial value (the tile's first MFMAs take it as C), so the
-//    epilogue is QuickGELU (c_fc) + conversion + stores, run in the wave's first read segment
-//    of the next tile, after that segment's fragment reads and staging issue; the stores are
-//    younger than the staged pieces the next waits count, which allow for them.
+//  * the epilogue (bias + QuickGELU for c_fc + conversion + stores) runs in the wave's first read
+//    segment of the next tile, after that segment's staging issue; its stores are younger than
+//    the staged pieces the next waits count, which allow for them. Its arithmetic is variant
+//    62's / the pipelined tiles' (acc from 0, + bias, x / (1 + __expf(-1.702 x))), so every tile
+//    gives the same bits and the tile choice (per shape, per lane split) never changes a result.
 //
 // Schedule. Slot = barrier interval. Group g's read segment of k-step t is slot 2t + g, its MFMA
 // segment slot 2t + g + 1 (group 1 runs one barrier behind). Stage s = t & 3 is read in slots 2t
@@ -155,7 +156,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         for (int fm = 0; fm < 8; ++fm)
 #pragma unroll
             for (int fn = 0; fn < 4; ++fn) {
-                acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fn][fm]);
             }
         __builtin_amdgcn_s_setprio(0);
     };
@@ -182,6 +183,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         int le;
         asm volatile("v_mov_b32 %0, %1" : "=v"(le) : "v"(lane));
         const int n = pn0 + wc * 64 + 16 * (le >> 4);
+        load_bias(pn0);  // the finished tile's bias slice
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
@@ -189,11 +191,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr];
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
             if constexpr (GELU) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
-                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.4554669595930156f * v[q]));
+                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x), as variant 62 / the pipelined tiles
+                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
             }
             u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
             u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
@@ -271,7 +273,6 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             if (have_prev) epilogue(pm0, pn0);
             else null_stores();
         }
-        if constexpr (decltype(first)::value) load_bias(n0);
         reads(stc);
         if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
         bar();

@@ -21,10 +21,11 @@
 //    stages W), and the tile-boundary crossing of the k-step stream is unrolled: the k-loop has
 //    no run-time branches; a missing next tile is a zero-length buffer resource (its pieces
 //    read as zeros into a stage nobody reads);
-//  * the bias is the accumulators' initial value (the tile's first MFMAs take it as C), so the
-//    epilogue is QuickGELU (c_fc) + conversion + stores, run in the wave's first read segment
-//    of the next tile, after that segment's fragment reads and staging issue; the stores are
-//    younger than the staged pieces the next waits count, which allow for them.
+//  * the epilogue (bias + QuickGELU for c_fc + conversion + stores) runs in the wave's first read
+//    segment of the next tile, after that segment's staging issue; its stores are younger than
+//    the staged pieces the next waits count, which allow for them. Its arithmetic is variant
+//    62's / the pipelined tiles' (acc from 0, + bias, x / (1 + __expf(-1.702 x))), so every tile
+//    gives the same bits and the tile choice (per shape, per lane split) never changes a result.
 //
 // Schedule. Slot = barrier interval. Group g's read segment of k-step t is slot 2t + g, its MFMA
 // segment slot 2t + g + 1 (group 1 runs one barrier behind). Stage s = t & 3 is read in slots 2t
@@ -207,7 +208,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                             asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[fn][fm]) : "a"(wf[fn]), "a"(af[fm]));
                     }
                 } else {
-                    acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? bv[fn] : acc[fn][fm]);
+                    acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fn][fm]);
                 }
             }
         __builtin_amdgcn_s_setprio(0);
@@ -239,10 +240,10 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         const int n = pn0 + wc * 64 + 16 * (le >> 4);
         if constexpr (AGP) {
             // the last MFMAs' AGPR results -> the v_accvgpr_reads below: 16 wait states (>= the 12
-            // an 8-pass XDL result needs), then this tile's bias slice
+            // an 8-pass XDL result needs)
             asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
-            load_bias(pn0);
         }
+        load_bias(pn0);  // the finished tile's bias slice
 #pragma unroll
         for (int fm = 0; fm < 8; ++fm) {
             const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
@@ -250,11 +251,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = AGP ? acc[f][fm][rr] + bv[f][rr] : acc[f][fm][rr];
+                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
             if constexpr (GELU) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x))
-                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.4554669595930156f * v[q]));
+                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x), as variant 62 / the pipelined tiles
+                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
             }
             u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
             u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
@@ -339,7 +340,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             else null_stores();
             hk.mark(ti, 1);
         }
-        if constexpr (decltype(first)::value && !AGP) load_bias(n0);
+
         if constexpr (!RF) reads(stc);
         if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
         bar(step, 0);
