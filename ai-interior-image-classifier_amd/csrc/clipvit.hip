@@ -249,11 +249,11 @@ struct clipvit_handle {
     // output + launch_quant_mx8 (same bytes; tuning attn_q8=0 restores the two kernels)
     bool attn_q8 = true;
     bool round_split = true;
-    // tiles of the two launches (0 = the role's); tuning split_variants. r05: the main launch on the
-    // 32-deep-k-step tile (72) with every pipelined role reading blocked weights (w_blk = 2): B/32
-    // bs 256 82.39-82.45k -> 82.68-82.94k img/s, 3 alternations on one box (c_proj 0.66 -> 0.65 ms
-    // per forward; profiles/r05/b32_wb2_split72_ab.txt)
-    int split_main = 72, split_tail = 81;
+    // tiles of the two launches (0 = the role's); tuning split_variants. r05: 72 as the main
+    // launch measured +0.3-0.6 % with the bias as its first MFMA's C (profiles/r05/
+    // b32_wb2_split72_ab.txt) and -0.3 % once its arithmetic was made v62's (bias in the epilogue,
+    // so that the tile choice never changes a result; profiles/r05/final_defaults_vs_r04.txt)
+    int split_main = 62, split_tail = 81;
     // XCD map of the main launch (tile_of_block; tuning split_xcd): 34 = the 1-D remap over a
     // column-group-major order with 2 N-groups, so each XCD group keeps half of W (2.4 MB of
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
@@ -264,8 +264,9 @@ struct clipvit_handle {
     // 16-B pieces, and c_proj's A k-tiles become contiguous 2 KB runs
     bool u_blk = true;
     // the Linear weights also in the 16-row blocked layout (GemmArgs.blk_w), read by: 2 = every
-    // launch whose tile reads it (default since r05, with split_main = 72), 1 = the launches on
-    // the 32-deep-k-step tiles only (72 / 74), 0 = none (no copies). tuning w_blocked
+    // launch whose tile reads it (default since r05; a row-split c_fc reads one copy in both of its
+    // launches), 1 = the launches on the 32-deep-k-step tiles only (72 / 74), 0 = none (no
+    // copies). tuning w_blocked
     int w_blk = 2;
 };
 
@@ -488,6 +489,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             const int tv = h->split_tail ? h->split_tail : variant;
             wsel(b, h->split_main);
             wsel(c, tv);
+            if (!b.blk_w) wsel(c, 0);  // both launches read one copy of W (the tail reuses the main's L2 lines)
             if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 && launch_gemm(s, h->dt, epi, c, tv) == 0)
                 return 0;
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);

@@ -395,8 +395,8 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu, x24):
 
 
 @pytest.mark.parametrize("name,dtype,B,tun", [
-    ("ViT-B/32", "fp16", 256, {}),              # c_fc: 32-deep-k-step v72 main + v81 tail; c_proj v82
-    ("ViT-B/32", "fp16", 256, {"split_variants": "62,81"}),  # the r04 ping-pong main
+    ("ViT-B/32", "fp16", 256, {}),              # c_fc: ping-pong v62 main + v81 tail; c_proj v82
+    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),  # the 32-deep-k-step main
     ("ViT-B/32", "bf16", 67, {}),               # one launch per role
     ("ViT-B/32", "fp16", 1, {}),                # M = 50: the last 16-row block is padding
     ("ViT-B/32", "fp16", 256, {"lnfold": 1}),   # EPI_LNF_GELU c_fc, EPI_RES_STATS c_proj
@@ -430,8 +430,8 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
 
 
 @pytest.mark.parametrize("name,dtype,B,tun", [
-    ("ViT-B/32", "fp16", 256, {}),                            # every B/32 role (v98, v72 + v81, v82) reads the copy (2)
-    ("ViT-B/32", "fp16", 256, {"split_variants": "62,81"}),   # the ping-pong main keeps row-major W
+    ("ViT-B/32", "fp16", 256, {}),                            # QKV v98, out / c_proj v82 read the copy (2); c_fc row-major
+    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),   # c_fc main 72 + tail 81 both read it
     ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}),          # one launch per role, ragged M
     ("ViT-B/16", "fp16", 64, {}),                             # N = 197, round split
     ("ViT-B/16", "fp16", 256, {}),                            # large M: every role on 3472 (default)
