@@ -266,7 +266,8 @@ struct clipvit_handle {
     // the Linear weights also in the 16-row blocked layout (GemmArgs.blk_w), read by: 2 = every
     // launch whose tile reads it (default since r05; a row-split c_fc reads one copy in both of its
     // launches), 1 = the launches on the 32-deep-k-step tiles only (72 / 74), 0 = none (no
-    // copies). tuning w_blocked
+    // copies). tuning w_blocked. B/32 bs 256: 87.2-87.4k -> 88.0-88.6k img/s against 0 (QKV 0.578 ->
+    // 0.565, c_proj 0.627 -> 0.610 ms per forward; same box, profiles/r05/b32_final_wblk_ab.txt)
     int w_blk = 2;
 };
 
