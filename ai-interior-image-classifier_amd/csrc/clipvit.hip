@@ -1273,7 +1273,9 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
-    const bool wblk = h->w_blk != 0 && !h->mx8;  // blocked weight copies of the four Linears
+    // blocked weight copies of the four Linears (MX-fp8: used by the bf16 blocks; the MX layers'
+    // copies stay unwritten and unread, gemm8 reads the packed e4m3 weights)
+    const bool wblk = h->w_blk != 0;
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         HIPCHK(alloc16(ly.wqkv, 3 * D * D));
