@@ -447,7 +447,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the blocked copy of W (w_blocked) for the launches whose tile reads it
     auto wsel = [&](GemmArgs& g, int v) {
         const bool blk = Wb && g.ksplit <= 1 &&
-                         (h->w_blk == 2 ? (v >= 8 && v != 62 && v != 63) : (h->w_blk == 1 && (v == 72 || v == 74)));
+                         (h->w_blk == 2 ? v >= 8 : (h->w_blk == 1 && (v == 72 || v == 74)));
         g.W = blk ? Wb : W;
         g.blk_w = blk;
     };

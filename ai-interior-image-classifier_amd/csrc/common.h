@@ -183,7 +183,7 @@ struct GemmArgs {
     int sc_rows;
     // W in the 16-row blocked layout (blk16_off over its packed rows, launch_blk16_relayout): a
     // 64-deep k-tile of 16 weight rows is one contiguous 2 KB run. Pipelined tiles (8..98, not the
-    // patch GEMM) and the 32-deep-k-step persistent tile (72) only.
+    // patch GEMM) and the persistent tiles (62 / 63 / 72 / 74) only.
     int blk_w;
     // EPI_RES_STATS: the residual x in 24-bit planes (x24_load / x24_store: C = the [M][ldc] u16
     // high plane, the byte plane at C + x24_plane); 0 = fp32 x at C

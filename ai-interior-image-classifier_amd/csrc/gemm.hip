@@ -880,8 +880,8 @@ int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int varian
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
-    // blocked W: the pipelined tiles and the 32-deep-k-step persistent tile
-    if (a.blk_w && (variant < 8 || variant == 62 || variant == 63 || a.ksplit > 1)) return -1;
+    // blocked W: the pipelined tiles and the persistent tiles (62 / 63 / 72 / 74)
+    if (a.blk_w && (variant < 8 || a.ksplit > 1)) return -1;
     if (variant == 62 || variant == 63 || variant == 72 || variant == 74) return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

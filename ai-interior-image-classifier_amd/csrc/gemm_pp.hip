@@ -40,7 +40,7 @@ namespace clipvit {
 // segment of the next tile while the other wave group's MFMAs go on. The bias vector of the
 // whole GEMM (N <= 8192) is parked in the 32 KB of LDS beside the two stages.
 
-template <typename T, int EPI, bool NT = false, bool BLKA = false>
+template <typename T, int EPI, bool NT = false, bool BLKA = false, bool BLKW = false>
 __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles) {
     typedef typename T::vec8 vec8;
     constexpr int BM = 256, BN = 256;
@@ -70,7 +70,9 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     // blocked A (blk_a, blk16_off; rows padded to 16): piece pc of the A stage is half pc & 1 of
     // 16-row block pc >> 1, whose k-tile run is contiguous — the LDS image is chunk-major
     // (BLKA compile-time: a runtime flag keeps both per-lane offset sets alive)
+    // blocked W (BLKW, GemmArgs.blk_w): the same form for the weight group's pieces
     const bool ablk = BLKA && grp == 0;
+    const bool oblk = ablk || (BLKW && grp == 1);  // this group's staged operand is blocked
     const int rows = grp == 0 ? (BLKA ? (a.M + 15) & ~15 : a.M) : a.N;
     auto rsrc_of = [&](int m0, int n0) {
         const int r0 = grp == 0 ? m0 : n0;
@@ -82,10 +84,10 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int pc = 8 * (i >> 1) + 2 * wc + (i & 1);
-        voff[i] = ablk ? (unsigned)((pc >> 1) * 16 * ldb + (pc & 1) * 1024 + lane * 16)
+        voff[i] = oblk ? (unsigned)((pc >> 1) * 16 * ldb + (pc & 1) * 1024 + lane * 16)
                        : (unsigned)((pc * 8 + lr) * ldb + chunk * 16);
     }
-    const int kstride = ablk ? 2048 : 128;  // bytes per k-tile along a row (block)
+    const int kstride = oblk ? 2048 : 128;  // bytes per k-tile along a row (block)
     const int opbase = grp == 0 ? 0 : A_BYTES;
 
     int m0, n0, mn = 0, nn = 0;
@@ -124,11 +126,13 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
     if (grp == 1) __builtin_amdgcn_s_barrier();  // the stagger
 
     const int lrow = lane & 15, lsw = lane & 7, lg = lane >> 4;
-    const int woff = A_BYTES + (wc * 64 + lrow) * 128;
-    const int c0 = ((0 | lg) ^ lsw) << 4, c1 = ((4 | lg) ^ lsw) << 4;
+    // W fragments: swizzled row-major image, or (BLKW) chunk-major 16-row blocks
+    const int woff = BLKW ? A_BYTES + wc * 64 * 128 + lrow * 16 : A_BYTES + (wc * 64 + lrow) * 128;
+    const int s0 = ((0 | lg) ^ lsw) << 4, s1 = ((4 | lg) ^ lsw) << 4;  // swizzled row-major chunks
+    const int c0 = BLKW ? lg << 8 : s0, c1 = BLKW ? (4 | lg) << 8 : s1;
     // A fragments: swizzled row-major image, or (blk_a) chunk-major 16-row blocks
     const int aoff = BLKA ? grp * 128 * 128 + lrow * 16 : (grp * 128 + lrow) * 128;
-    const int a0 = BLKA ? lg << 8 : c0, a1 = BLKA ? (4 | lg) << 8 : c1;
+    const int a0 = BLKA ? lg << 8 : s0, a1 = BLKA ? (4 | lg) << 8 : s1;
     vec8 af[4][2], wf[4][2];
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
 
@@ -297,7 +301,14 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
     if (a.blk_a) {  // blocked A (u): c_proj on the persistent tile (tuning / large-M shapes)
-        if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+        if (epi != EPI_STORE) return -1;
+        if (a.blk_w) gemm_ppp_kernel<T, EPI_STORE, NT, true, true><<<grid, 512, 0, s>>>(a, ntiles);
+        else gemm_ppp_kernel<T, EPI_STORE, NT, true><<<grid, 512, 0, s>>>(a, ntiles);
+        return 0;
+    }
+    if (a.blk_w) {  // blocked W
+        if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, false, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+        if (epi == EPI_GELU) { gemm_ppp_kernel<T, EPI_GELU, NT, false, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
         return -1;
     }
     if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }

@@ -34,7 +34,7 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # gemm_p32.h; 74 the same with non-temporal stores); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
 # 2xx = the production XCD partition.
 VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 74, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472, 3474, 3480,
-            10008, 10022, 10072, 10080, 10081, 10082, 10090, 10098, 13472]
+            10008, 10022, 10062, 10063, 10072, 10080, 10081, 10082, 10090, 10098, 13462, 13472]
 N128 = (1, 2, 22, 81, 82)
 N256 = (3, 8, 62, 63, 72, 74, 80, 98)
 STAGED = (62, 63, 72, 74, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
@@ -222,7 +222,7 @@ def test_attention_tail_rows_never_read(gpu, B, N, H, causal):
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
                                    (36928 // 4, 4096, 1024)])
 def test_ping_pong_race_screen(gpu, M, N, K):
-    """The persistent ping-pong GEMMs (62, 63) hand LDS stages between waves by counted vmcnt and
+    """The persistent ping-pong GEMMs (62, 63; + 10000 with the blocked weight copy) hand LDS stages between waves by counted vmcnt and
     barriers only. Every accumulator sees the same k order as the 2-phase 256x256 tile (v8), so
     the outputs must equal v8's bit for bit on every one of many repeated launches: a read that
     overtook its DMA (or a refill that overtook a read) would show as a differing tile."""
@@ -232,7 +232,7 @@ def test_ping_pong_race_screen(gpu, M, N, K):
     bias = torch.randn(N, device=gpu, generator=g)
     for epi in (10, 11):  # 16-bit store / QuickGELU
         ref = E.gemm_test(A, W, bias, epi=epi, variant=8)
-        for variant in (62, 63, 3462, 3463):
+        for variant in (62, 63, 3462, 3463, 10062, 13462, 13463):  # + 10000: blocked weight copy
             for _ in range(6):
                 C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
