@@ -32,6 +32,9 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}"
 # +0.5 %, L/14@336 +0.7 / +1.0 % img/s, patch GEMM -7 %; on attention.hip it cost 6 %, so
 # only the GEMMs get it.
 SRC_FLAGS = {"gemm": ["-mllvm", "--amdgpu-sched-strategy=max-memory-clause"]}
+# gemm_w4.hip (one wave per SIMD, 256 accumulators per lane): its accumulators must be AGPRs,
+# so it is built without --amdgpu-mfma-vgpr-form
+SRC_DROP = {"gemm_w4": ["--amdgpu-mfma-vgpr-form"]}
 
 
 def _sources() -> list[Path]:
@@ -50,7 +53,11 @@ def _compile(src: Path) -> tuple[Path, str]:
     deps = [src, *CSRC.glob("*.h"), INCLUDE / "clipvit.h", Path(__file__)]  # this file: the flags
     if not _needs(obj, deps):
         return obj, ""
-    cmd = [HIPCC, *CFLAGS, *SRC_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)]
+    flags = list(CFLAGS)
+    for f in SRC_DROP.get(src.stem, []):  # a dropped -mllvm option takes its -mllvm with it
+        i = flags.index(f)
+        del flags[i - 1:i + 1]
+    cmd = [HIPCC, *flags, *SRC_FLAGS.get(src.stem, []), "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stdout}\n{r.stderr}")
