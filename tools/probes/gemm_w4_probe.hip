@@ -1,6 +1,9 @@
-// Persistent 256x256 MFMA GEMM with ONE wave per SIMD (variants 76 / 77; round 5). Its own
-// translation unit: built without --amdgpu-mfma-vgpr-form (build.py), so the 256 accumulators
-// per lane live in AGPRs.
+// PROBE (not built into the library): persistent 256x256 MFMA GEMM with ONE wave per SIMD (r05
+// variants 76 / 77). Bit-identical to variant 8 on the race screen, and 5-15 % slower than
+// variant 72 on every measured shape (profiles/r05/w4_probe.txt), so it was removed from the
+// build. To re-measure it: restore the variant 76 / 77 routing of launch_gemm_pp (git history),
+// compile this file without --amdgpu-mfma-vgpr-form (its 256 accumulators per lane must be
+// AGPRs) and link it with the library objects.
 //
 //   C[M, N] = A[M, K] @ W[N, K]^T + bias   (16-bit C; QuickGELU for c_fc)
 //
