@@ -34,7 +34,7 @@
 
 #include "common.h"
 
-// schedule knobs (probe builds: tools/r05_w4_knobs.sh)
+// schedule knobs (probe builds: tools/r05_runs.sh w4_knobs)
 #ifndef W4_FRONT
 #define W4_FRONT 0  // 1: a k-step's 8 staging pieces issued before its MFMAs, not interleaved
 #endif

@@ -1,4 +1,4 @@
-"""Host-only: per-kernel median PMC values from the rocprofv3 .db files of tools/r05_pmc.sh
+"""Host-only: per-kernel median PMC values from the rocprofv3 .db files of tools/r05_runs.sh pmc
 (gpurun_out/r05_pmc/k<kind>/p<pass>/) -> a markdown table on stdout."""
 import collections
 import glob
