@@ -32,9 +32,8 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}"
 # +0.5 %, L/14@336 +0.7 / +1.0 % img/s, patch GEMM -7 %; on attention.hip it cost 6 %, so
 # only the GEMMs get it.
 SRC_FLAGS = {"gemm": ["-mllvm", "--amdgpu-sched-strategy=max-memory-clause"]}
-# gemm_w4.hip (one wave per SIMD, 256 accumulators per lane): its accumulators must be AGPRs,
-# so it is built without --amdgpu-mfma-vgpr-form
-SRC_DROP = {"gemm_w4": ["--amdgpu-mfma-vgpr-form"]}
+# options a unit is built without (none since the r05 one-wave-per-SIMD probes left the build)
+SRC_DROP: dict[str, list[str]] = {}
 
 
 def _sources() -> list[Path]:

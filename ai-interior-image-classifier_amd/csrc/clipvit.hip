@@ -447,7 +447,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // the blocked copy of W (w_blocked) for the launches whose tile reads it
     auto wsel = [&](GemmArgs& g, int v) {
         const bool blk = Wb && g.ksplit <= 1 &&
-                         (h->w_blk == 2 ? v >= 8 : (h->w_blk == 1 && (v == 72 || v == 74 || v == 76 || v == 77)));
+                         (h->w_blk == 2 ? v >= 8 : (h->w_blk == 1 && (v == 72 || v == 74)));
         g.W = blk ? Wb : W;
         g.blk_w = blk;
     };
@@ -1131,7 +1131,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72 || m[0] == 74 || m[0] == 76);
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72 || m[0] == 74);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
@@ -1603,7 +1603,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 72 || variant == 74 || variant == 76 || variant == 77;
+                        variant == 63 || variant == 72 || variant == 74;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

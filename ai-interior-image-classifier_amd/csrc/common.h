@@ -335,7 +335,6 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
 // ping-pong 256x256 GEMM (gemm_pp.hip): variant 60 direct stores, 61 LDS-staged stores;
 // EPI_STORE / EPI_GELU, N % 256 == 0, K % 128 == 0
-int launch_gemm_w4(hipStream_t s, int dtype, int epi, const GemmArgs& a, bool nt);  // gemm_w4.hip
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
 // implicit-GEMM patch embedding (no im2col): P = patch size (14, 16, 32), a.A = pixels
 int launch_patch_gemm(hipStream_t s, int dtype, int P, const GemmArgs& a);

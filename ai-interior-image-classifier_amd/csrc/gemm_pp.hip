@@ -348,7 +348,6 @@ int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int var
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     if (variant == 72 || variant == 74)
         return dtype == 2 ? launch_p32<F16>(s, epi, a, variant == 74) : launch_p32<BF16>(s, epi, a, variant == 74);
-    if (variant == 76 || variant == 77) return launch_gemm_w4(s, dtype, epi, a, variant == 77);
     return -1;
 }
 

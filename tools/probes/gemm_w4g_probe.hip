@@ -1,6 +1,8 @@
-// Persistent 256x256 MFMA GEMM with ONE wave per SIMD and register-staged operands (variant 76;
-// round 5 probe). Its own translation unit: built without --amdgpu-mfma-vgpr-form (build.py), so
-// the 256 accumulators per lane live in AGPRs.
+// PROBE (not built into the library): persistent 256x256 MFMA GEMM with ONE wave per SIMD and
+// register-staged operands (r05 variant 76, second form). Bit-identical to variant 8, and slower
+// than both the LDS-DMA form (gemm_w4_probe.hip) and variant 72 (profiles/r05/w4_probe.txt). To
+// re-measure: restore the variant 76 / 77 routing (commit 1a6b0fe) and build this file without
+// --amdgpu-mfma-vgpr-form (its 256 accumulators per lane must be AGPRs).
 //
 //   C[M, N] = A[M, K] @ W[N, K]^T + bias   (16-bit C; QuickGELU for c_fc)
 //
