@@ -339,8 +339,8 @@ static int launch_p32(hipStream_t s, int epi, const GemmArgs& a, bool nt) {
 
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
 // non-temporal stores (the large-M roles of B/16 and L/14@336); 72: the 32-deep-k-step
-// persistent tile of gemm_p32.h (GemmArgs.blk_w: W in the 16-row blocked layout, every staged
-// k-step of a 16-row block one contiguous 1 KB run); 74: 72 with non-temporal stores
+// persistent tile of gemm_p32.h; 74: 72 with non-temporal stores. GemmArgs.blk_w (all four): W
+// in the 16-row blocked layout, every staged k-tile of a 16-row block one contiguous run.
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
     if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
