@@ -1145,11 +1145,12 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         ok = parse_int(v, x);
         if (ok) h->split_min = x <= 0 ? SPLIT_NEVER : x;
     } else if (k == "gemm_xcd") ok = parse_list(v, h->xcd, 5);
-    else if (k == "qkv_variant") {  // 100 * XCD map + tile of the QKV role, shape rules kept (gemm_variants forces all)
-        ok = parse_int(v, x) && x > 0;
+    else if (k == "qkv_variant" || k == "fc_variant") {  // 100 * XCD map + tile of the QKV / c_fc role,
+        ok = parse_int(v, x) && x > 0;                    // shape rules kept (gemm_variants forces all)
+        const int r = k == "qkv_variant" ? R_QKV : R_FC;
         if (ok) {
-            h->var[R_QKV] = x % 100;
-            h->xcd[R_QKV] = x / 100;
+            h->var[r] = x % 100;
+            h->xcd[r] = x / 100;
         }
     }
     else if (k == "mx8_skip") {  // both masks
@@ -1603,7 +1604,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 72 || variant == 74;
+                        variant == 63 || variant == 72 || variant == 74 || variant == 75;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

@@ -882,7 +882,8 @@ int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int varian
     }
     // blocked W: the pipelined tiles and the persistent tiles (62 / 63 / 72 / 74)
     if (a.blk_w && (variant < 8 || a.ksplit > 1)) return -1;
-    if (variant == 62 || variant == 63 || variant == 72 || variant == 74) return launch_gemm_pp(s, dtype, epi, a, variant);
+    if (variant == 62 || variant == 63 || variant == 72 || variant == 74 || variant == 75)
+        return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;
     if (dtype == 2) return launch_t<F16>(s, epi, a, variant);

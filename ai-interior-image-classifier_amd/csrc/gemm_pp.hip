@@ -317,11 +317,12 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
 }
 
 template <typename T, bool BLKW, bool NT>
-static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a) {
+static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a, bool balanced = false) {
     if (a.K % 128 || a.K < 256) return -1;  // whole groups of four 32-deep k-steps, >= 2 groups
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
-    const int grid = ntiles < ncu ? ntiles : ncu;
+    const int per = (ntiles + ncu - 1) / ncu;
+    const int grid = balanced ? (ntiles + per - 1) / per : ntiles < ncu ? ntiles : ncu;
     if (a.blk_a) {  // blocked A (u): c_proj
         if (epi == EPI_STORE) { gemm_p32_kernel<T, EPI_STORE, true, BLKW, NT><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
         return -1;
@@ -332,14 +333,15 @@ static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a) {
 }
 
 template <typename T>
-static int launch_p32(hipStream_t s, int epi, const GemmArgs& a, bool nt) {
-    if (nt) return a.blk_w ? launch_p32_t<T, true, true>(s, epi, a) : launch_p32_t<T, false, true>(s, epi, a);
-    return a.blk_w ? launch_p32_t<T, true, false>(s, epi, a) : launch_p32_t<T, false, false>(s, epi, a);
+static int launch_p32(hipStream_t s, int epi, const GemmArgs& a, bool nt, bool bal = false) {
+    if (nt) return a.blk_w ? launch_p32_t<T, true, true>(s, epi, a, bal) : launch_p32_t<T, false, true>(s, epi, a, bal);
+    return a.blk_w ? launch_p32_t<T, true, false>(s, epi, a, bal) : launch_p32_t<T, false, false>(s, epi, a, bal);
 }
 
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
 // non-temporal stores (the large-M roles of B/16 and L/14@336); 72: the 32-deep-k-step
-// persistent tile of gemm_p32.h; 74: 72 with non-temporal stores. GemmArgs.blk_w (all four): W
+// persistent tile of gemm_p32.h; 74: 72 with non-temporal stores; 75: 72 on a balanced grid (600
+// tiles on 200 workgroups x 3, as hipBLASLt sizes c_fc; tuning fc_variant). GemmArgs.blk_w: W
 // in the 16-row blocked layout, every staged k-tile of a 16-row block one contiguous run.
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
@@ -348,6 +350,8 @@ int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int var
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     if (variant == 72 || variant == 74)
         return dtype == 2 ? launch_p32<F16>(s, epi, a, variant == 74) : launch_p32<BF16>(s, epi, a, variant == 74);
+    if (variant == 75)  // 72 on the fewest workgroups with the same tiles per workgroup (tuning only)
+        return dtype == 2 ? launch_p32<F16>(s, epi, a, false, true) : launch_p32<BF16>(s, epi, a, false, true);
     return -1;
 }
 
