@@ -27,6 +27,7 @@ EXPORTS = (
     "clipvit_gemm_mx8_test", "clipvit_preprocess", "clipvit_resample_plan",
     "clipvit_text_create", "clipvit_text_load_weights", "clipvit_text_load_lora",
     "clipvit_encode_text", "clipvit_text_destroy", "clipvit_residual_x24_test", "clipvit_set_tuning",
+    "clipvit_gemm_log",
 )
 
 
@@ -96,6 +97,7 @@ def lib() -> ctypes.CDLL:
             "clipvit_quant_mx8_test": (i, [vp, i, vp, i, i, vp, vp]),
             "clipvit_gemm_mx8_test": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, i, i, i]),
             "clipvit_profile_forward": (i, [vp, vp, vp, i, i, i, p_f]),
+            "clipvit_gemm_log": (i, [vp, ctypes.POINTER(i), i]),
             "clipvit_gemm_bench": (i, [i, i, i, i, i, i, i, p_f]),
             "clipvit_text_create": (i, [ctypes.POINTER(TextConfig), i, ctypes.POINTER(vp)]),
             "clipvit_text_load_weights": (i, [vp, ctypes.POINTER(Tensor), ctypes.c_size_t]),

@@ -272,7 +272,21 @@ struct clipvit_handle {
     // copies). tuning w_blocked. B/32 bs 256: 87.2-87.4k -> 88.0-88.6k img/s against 0 (QKV 0.578 ->
     // 0.565, c_proj 0.627 -> 0.610 ms per forward; same box, profiles/r05/b32_final_wblk_ab.txt)
     int w_blk = 2;
+    // test hook (tuning trace_gemm=1): every role GEMM launch of gemm() / gemm8() appends
+    // {role, tile variant, M, flags} here (clipvit_gemm_log), so a test can assert which kernel
+    // path a configuration reaches. Off in the product path.
+    bool trace = false;
+    std::mutex trace_mu;
+    std::vector<int> trace_log;
+    void log_launch(int role, int variant, int M, int flags) {
+        if (!trace) return;
+        std::lock_guard<std::mutex> lk(trace_mu);
+        trace_log.insert(trace_log.end(), {role, variant, M, flags});
+    }
 };
+
+// flags of a clipvit_gemm_log entry
+enum { LOG_BLK_W = 1, LOG_MX8 = 2, LOG_BLK_A = 4, LOG_BLK_C = 8 };
 
 static std::string L(int i, const char* leaf) {
     return "visual.transformer.resblocks." + std::to_string(i) + "." + leaf;
@@ -447,6 +461,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     a.blk_c = ublk && role == R_FC;
     a.blk_a = ublk && role == R_PROJ;
     int variant = h->var[role];
+    auto launch = [&](const GemmArgs& g, int v) {
+        const int rc = launch_gemm(s, h->dt, epi, g, v);
+        if (rc == 0)
+            h->log_launch(role, v, g.M, (g.blk_w ? LOG_BLK_W : 0) | (g.blk_a ? LOG_BLK_A : 0) | (g.blk_c ? LOG_BLK_C : 0));
+        return rc;
+    };
     // the blocked copy of W (w_blocked) for the launches whose tile reads it
     auto wsel = [&](GemmArgs& g, int v) {
         const bool blk = Wb && g.ksplit <= 1 &&
@@ -457,12 +477,12 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // Large-M shapes (L/14@336: M = 73,856; B/16): with several rounds of 256x256 tiles the
     // quantization loss that made the smaller tiles win at B/32 is gone and the 256x256 tile's
     // lower LDS fill per FLOP wins — measured: config 4 1,918 -> 2,072 img/s; B/16 c_fc (2,364
-    // tiles) and out/c_proj (591 tiles, N = 768 roles from 2 rounds) 19.3k -> 20.2k img/s;
-    // B/32's c_fc (600 tiles) stays faster on 128x128.
+    // tiles) and out/c_proj (591 tiles, N = 768 roles from 2 rounds) 19.3k -> 20.2k img/s.
+    // B/32's c_fc (600 tiles) takes the balanced v75 launch above instead.
     const long t256 = N % 256 == 0 ? (long)((M + 255) / 256) * (N / 256) : 0;
     // Whole-round row split (QKV / c_fc, 16-bit outputs). When the 256x256 tiles of a shape fill
-    // R whole rounds of the CUs plus a remainder of at most half a round (B/32 c_fc at bs 256:
-    // 600 tiles = 2 rounds + 88), rows [0, M1) — the most 256-row tiles that fit in R rounds,
+    // R whole rounds of the CUs plus a remainder of at most half a round (B/32 c_fc at bs 128:
+    // 300 tiles = 1 round + 44), rows [0, M1) — the most 256-row tiles that fit in R rounds,
     // 1-D block map so every XCD gets the same tile count — run on 256x256 tiles and rows
     // [M1, M) on the role's small tile as a second launch. Row-wise independent outputs:
     // bit-identical to one launch. Measured (c_fc 12800 x 3072 x 768): 81.6 us in one launch
@@ -487,7 +507,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             // profiles/r05/balanced_grid_probe.txt)
             a.xcd_n = h->split_xcd;
             wsel(a, 75);
-            if (launch_gemm(s, h->dt, epi, a, 75) == 0) return 0;
+            if (launch(a, 75) == 0) return 0;
             wsel(a, 0);
             a.xcd_n = h->xcd[role];
         }
@@ -506,7 +526,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             wsel(b, h->split_main);
             wsel(c, tv);
             if (!b.blk_w) wsel(c, 0);  // both launches read one copy of W (the tail reuses the main's L2 lines)
-            if (launch_gemm(s, h->dt, epi, b, h->split_main) == 0 && launch_gemm(s, h->dt, epi, c, tv) == 0)
+            if (launch(b, h->split_main) == 0 && launch(c, tv) == 0)
                 return 0;
             g_err = "gemm: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
@@ -526,9 +546,9 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     }
     // a tuned variant that does not tile this shape falls back to the shape-based choice
     wsel(a, variant);
-    int rc = launch_gemm(s, h->dt, epi, a, variant);
+    int rc = launch(a, variant);
     wsel(a, 0);
-    if (rc != 0 && launch_gemm(s, h->dt, epi, a, 0) != 0) {
+    if (rc != 0 && launch(a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
                 " K=" + std::to_string(K);
         return CLIPVIT_E_INVALID;
@@ -582,6 +602,11 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
     a.xcd_n = h->xcd[role];
     a.ncu = h->ncu;
     const int v8 = h->var8[role];
+    auto launch = [&](const GemmArgs& g, int v) {
+        const int rc = launch_gemm_mx8(s, CLIPVIT_BF16, epi, g, v);
+        if (rc == 0) h->log_launch(role, v, g.M, LOG_MX8 | (g.blk_a ? LOG_BLK_A : 0) | (g.blk_c ? LOG_BLK_C : 0));
+        return rc;
+    };
     if (v8 == 3 && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
     // Whole-round row split of the MX c_fc (as gemm()'s for the 16-bit one): when the 256x256
     // tiles fill R whole rounds plus at most half a round (B/32 lane of 256 images: 600 tiles =
@@ -601,15 +626,13 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
             c.C = (unsigned char*)C + (size_t)m1 * ldc;  // = blk8_off(m1, 0, ldc): m1 % 16 == 0
             c.sC = a.sC + (a.sc_rows ? (size_t)m1 * 4 : (size_t)m1 * (ldc / 32));
             c.xcd_n = 0;
-            if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, b, 3) == 0 &&
-                launch_gemm_mx8(s, CLIPVIT_BF16, epi, c, h->mx8_split_tail) == 0)
+            if (launch(b, 3) == 0 && launch(c, h->mx8_split_tail) == 0)
                 return 0;
             g_err = "gemm8: round split failed M=" + std::to_string(M) + " N=" + std::to_string(N);
             return CLIPVIT_E_INVALID;
         }
     }
-    if (launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, v8) != 0 &&
-        launch_gemm_mx8(s, CLIPVIT_BF16, epi, a, 0) != 0) {
+    if (launch(a, v8) != 0 && launch(a, 0) != 0) {
         g_err = "gemm8: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
                 " K=" + std::to_string(K);
         return CLIPVIT_E_INVALID;
@@ -763,8 +786,10 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
 // Class-token tail of the last block on the LayerNorm-fold path (see cls_tail): the gathered
 // CLS rows go through the same per-row arithmetic as the full block — out_proj on the full-M
 // out_proj tile (160x128, EPI_RES_STATS: x += ., x16, the 128-column statistics in the same
-// order), c_fc with the folded ln_2, c_proj (+x, fp32) — so the features equal the unpruned
-// forward's bit for bit; then ln_post @ proj.
+// order), c_fc with the folded ln_2, c_proj (+x, fp32); then ln_post @ proj. On fp32 x the
+// features equal the unpruned forward's bit for bit; on the 24-bit residual planes they do not
+// (the tail keeps the CLS rows of x in fp32, where the full block would re-round them to 24 bits),
+// and the fold's tests hold them to the oracle bar instead.
 static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_out, Prof* prof,
                          const void* x24 = nullptr) {
     const int D = h->D, N = h->N, np = D / 128;
@@ -1144,6 +1169,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
+    else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
@@ -1204,14 +1230,14 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
         int w_blk, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->w_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->w_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1227,7 +1253,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->w_blk = before.w_blk;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->w_blk = before.w_blk;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1290,8 +1316,9 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
-    // blocked weight copies of the four Linears (MX-fp8: used by the bf16 blocks; the MX layers'
-    // copies stay unwritten and unread, gemm8 reads the packed e4m3 weights)
+    // blocked weight copies of the Linears that pack_linear re-lays out: not for the MX-fp8 roles
+    // (gemm8 reads the packed e4m3 weights) nor for the LayerNorm-folded QKV / c_fc (their fold
+    // branch packs the row-major operand only)
     const bool wblk = h->w_blk != 0;
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
@@ -1299,10 +1326,12 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
         HIPCHK(alloc16(ly.wout, D * D));
         HIPCHK(alloc16(ly.wfc, 4 * D * D));
         HIPCHK(alloc16(ly.wproj, 4 * D * D));
-        if (wblk) {
-            HIPCHK(alloc16(ly.wqkv_b, 3 * D * D));
-            HIPCHK(alloc16(ly.wfc_b, 4 * D * D));
+        if (wblk && !h->q8_attn(i)) {
+            if (!h->lnfold) HIPCHK(alloc16(ly.wqkv_b, 3 * D * D));
             HIPCHK(alloc16(ly.wout_b, D * D));
+        }
+        if (wblk && !h->q8_mlp(i)) {
+            if (!h->lnfold) HIPCHK(alloc16(ly.wfc_b, 4 * D * D));
             HIPCHK(alloc16(ly.wproj_b, 4 * D * D));
         }
         ly.bqkv = h->master[L(i, "attn.in_proj_bias")];
@@ -1491,6 +1520,16 @@ int clipvit_classify(clipvit_handle* h, void* stream, const void* pixels_dev, in
     return rc;
 }
 
+int clipvit_gemm_log(clipvit_handle* h, int* out, int cap) {
+    g_err.clear();
+    if (!h || (!out && cap > 0) || cap < 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(h->trace_mu);
+    const int n = std::min(cap, (int)(h->trace_log.size() / 4));
+    if (n) memcpy(out, h->trace_log.data(), (size_t)n * 4 * sizeof(int));
+    h->trace_log.clear();
+    return n;
+}
+
 int clipvit_profile_forward(clipvit_handle* h, void* stream, const void* pixels_dev, int dtype, int B,
                             int iters, float* out_ms) {
     g_err.clear();
@@ -1602,6 +1641,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     launch_pack_weight(s, dtype, (const float*)W_dev, Wp, N, K, K);
     const bool wblk = variant >= 10000;  // + 10000: W in the blocked layout (GemmArgs.blk_w)
     variant %= 10000;
+    if (wblk && N % 16) FAIL(CLIPVIT_E_INVALID, "blocked W needs N % 16 == 0");
     if (wblk) {  // relayout in place through a copy
         void* Wr = nullptr;
         HIPCHK(hipMallocAsync(&Wr, (size_t)N * K * 2, s));
@@ -1721,6 +1761,7 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.patch_g2 = 49; a.patch_ntok = 50;
     a.blk_w = variant >= 10000;  // (random operands: the layout only changes the access pattern)
     variant %= 10000;
+    if (a.blk_w && N % 16) FAIL(CLIPVIT_E_INVALID, "blocked W needs N % 16 == 0");
     a.xcd_n = variant / 100;
     variant %= 100;
     a.ncu = current_ncu();

@@ -255,8 +255,9 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     };
     //
     // one k-step (compile-time position): ST / STI = stage read / staged; NXT = the staged step
-    // belongs to the next tile (kk = step within that tile); FIRST = the tile's first step (bias
-    // as the accumulators' initial value); EP = it carries the previous tile's epilogue; W24 =
+    // belongs to the next tile (kk = step within that tile); FIRST = the tile's first step (its
+    // MFMAs start the accumulators from 0; the bias is added in the epilogue); EP = it carries the
+    // previous tile's epilogue; W24 =
     // wait allowance 24 instead of 8
     auto kstep = [&](int step, int kk_issue, auto nxt, auto stc, auto stic, auto first, auto ep, auto w24,
                      bool have_prev, int pm0, int pn0) {

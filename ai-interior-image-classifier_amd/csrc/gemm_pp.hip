@@ -350,7 +350,7 @@ int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int var
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     if (variant == 72 || variant == 74)
         return dtype == 2 ? launch_p32<F16>(s, epi, a, variant == 74) : launch_p32<BF16>(s, epi, a, variant == 74);
-    if (variant == 75)  // 72 on the fewest workgroups with the same tiles per workgroup (tuning only)
+    if (variant == 75)  // 72 on the fewest workgroups with the same tiles per workgroup (the B/32 bs-256 c_fc)
         return dtype == 2 ? launch_p32<F16>(s, epi, a, false, true) : launch_p32<BF16>(s, epi, a, false, true);
     return -1;
 }

@@ -658,7 +658,7 @@ void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, i
 }
 
 // Row-major 16-bit [rows, cols] -> the 16-row blocked layout (blk16_off; rows % 16 == 0,
-// cols % 64 == 0): the weight operand of GEMM variant 73. One thread per 16-B chunk.
+// cols % 64 == 0): the blocked weight copies (GemmArgs.blk_w) and blocked u. One thread per 16-B chunk.
 __global__ void blk16_relayout_kernel(const uint4* __restrict__ src, unsigned char* __restrict__ dst, int rows,
                                       int cols) {
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -197,6 +197,16 @@ class VisionEngine:
         out["event_gap_ms"] = float(ms[19])
         return out
 
+    def gemm_log(self, cap: int = 4096) -> list[tuple[int, int, int, int]]:
+        """Test hook: the (role, tile variant, M, flags) of every Linear-role GEMM launch since the
+        last call (needs tuning trace_gemm=1; clipvit_gemm_log). Roles: 0 qkv, 1 out_proj, 2 c_fc,
+        3 c_proj; flags: 1 blocked W copy, 2 MX-fp8, 4 blocked A, 8 blocked C."""
+        buf = (ctypes.c_int * (4 * cap))()
+        n = self._L.clipvit_gemm_log(self._h, buf, cap)
+        if n < 0:
+            _lib.check(n)
+        return [tuple(buf[4 * i:4 * i + 4]) for i in range(n)]
+
 
 # ------------------------------------------------------------------ kernel-level helpers
 def gemm_test(A: torch.Tensor, W: torch.Tensor, bias: torch.Tensor | None, epi: int = 0,

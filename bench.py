@@ -3,6 +3,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+Both forms run N ranks: without a torchrun environment, --gpus N > 1 starts the N rank processes
+itself (launch_ranks) and relays rank 0's line; under torchrun, WORLD_SIZE must equal --gpus.
+
 A step = one ``classify`` of a resident synthetic batch (ViT-B/32 + merged LoRA r=8, fp16 MFMA operands,
 224x224 fp32 pixels as preprocess returns them, 256 images per GPU): patch-embed -> 12 blocks -> ln_post/proj -> L2-norm -> 100*cos
 logits over 437 labels -> segment softmax + top-5, followed (N > 1) by the RCCL all-gather of
@@ -23,23 +26,80 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
 
-import torch
-import torch.distributed as dist
-
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
-import amd_pkg  # noqa: E402
 
-amd_pkg.load()
-from interior_amd import config as C  # noqa: E402
-from interior_amd.dp import allgather_rows, env_rank  # noqa: E402
-from interior_amd.engine import VisionEngine  # noqa: E402
-from interior_amd.lora import synthetic_adapters  # noqa: E402
-from interior_amd.weights import synthetic_state_dict  # noqa: E402
+# The engine (and with it torch / the HIP library) is imported by _import_engine() only in the
+# process that runs a rank: the parent of a self-launched N-rank run (launch_ranks) never loads
+# the GPU stack, so no GPU state exists in it when it starts the rank processes.
+torch = dist = C = allgather_rows = VisionEngine = synthetic_adapters = synthetic_state_dict = None
+
+
+def _import_engine():
+    global torch, dist, C, allgather_rows, VisionEngine, synthetic_adapters, synthetic_state_dict
+    import torch as _torch
+    import torch.distributed as _dist
+
+    import amd_pkg
+    amd_pkg.load()
+    from interior_amd import config as _C
+    from interior_amd.dp import allgather_rows as _ag
+    from interior_amd.engine import VisionEngine as _VE
+    from interior_amd.lora import synthetic_adapters as _sa
+    from interior_amd.weights import synthetic_state_dict as _ssd
+    torch, dist, C, allgather_rows = _torch, _dist, _C, _ag
+    VisionEngine, synthetic_adapters, synthetic_state_dict = _VE, _sa, _ssd
+
+
+def world_from_env() -> tuple[int, int, int]:
+    """(rank, local_rank, world_size) from the torchrun environment (1-process defaults)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv: list[str]) -> int:
+    """`python bench.py --gpus N` (N > 1) outside torchrun: start the N rank processes as
+    `python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+    bench.py <same arguments>` (children, so this process never touches the GPU), pass their
+    stderr through, and relay rank 0's one JSON line after checking that it reports N ranks
+    (and, unless --share-gpu, an RCCL world of N whose gather check passed). Exit status: the
+    launcher's, or 3 when the line is missing or reports another world."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    for l in r.stdout.splitlines():
+        if not l.startswith("{"):
+            print(l, file=sys.stderr)
+    if r.returncode != 0:
+        print(f"[bench] rank processes exited with {r.returncode}", file=sys.stderr, flush=True)
+        return r.returncode
+    if len(lines) != 1:
+        print(f"[bench] expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr, flush=True)
+        return 3
+    d = json.loads(lines[0])
+    ok = d.get("ranks") == a.gpus and d.get("rccl_world") == a.gpus and d.get("gather_ok") is True
+    if not a.share_gpu:
+        ok = ok and d.get("n_gpus") == a.gpus and d.get("backend") == "nccl"
+    print(lines[0], flush=True)
+    if not ok:
+        print(f"[bench] the line does not report {a.gpus} ranks with a verified all-gather", file=sys.stderr, flush=True)
+        return 3
+    return 0
 
 PEAK_TFLOPS = {"bf16": 2516.6, "fp16": 2516.6, "mxfp8": 5033.2}  # dense MFMA peaks (MI355X_MICROARCH.md)
 N_CLASSES = 437
@@ -252,7 +312,14 @@ def reconcile(fam: dict, step_ms: float):
 
 def main():
     a = parse()
-    rank, local_rank, world = env_rank()
+    rank, local_rank, world = world_from_env()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
+    if world != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(python bench.py --gpus N starts them itself)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    _import_engine()
     # --share-gpu: every rank on cuda:0 (rehearsal of the N-rank code path on a 1-GPU box;
     # RCCL refuses two ranks on one device, so that mode uses gloo for the all-gather)
     gpu_index = 0 if a.share_gpu else local_rank

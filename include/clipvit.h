@@ -29,8 +29,9 @@ extern "C" {
 /* 2: clipvit_attention_test takes `causal` (8 arguments; version 1 had 7), and
  *    clipvit_profile_forward writes 20 floats to out_ms (version 1 wrote 10: a version-1 caller's
  *    10-float buffer overflows).
- * 3: clipvit_set_tuning (the library reads no environment variables). */
-#define CLIPVIT_ABI_VERSION 3
+ * 3: clipvit_set_tuning (the library reads no environment variables).
+ * 4: clipvit_gemm_log (test hook). */
+#define CLIPVIT_ABI_VERSION 4
 
 /* Status codes. */
 #define CLIPVIT_OK 0
@@ -102,11 +103,19 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * split_variants "main,tail"; tail_variant; tail_kmin (>= 64, multiple of 64) / tail_smax (1..48):
  * the class-token tail's split-K rule; head_cols (64 / 32); mx8_split_tail (0, 2, 5);
  * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
- * qkv_variant (100 * XCD map + tile of the QKV role only);
+ * qkv_variant / fc_variant (100 * XCD map + tile of the QKV / c_fc role only); fc_balanced (0/1:
+ * c_fc with >= 2 whole rounds of 256x256 tiles plus a remainder as one balanced launch, default 1,
+ * or as the round split of split_variants); trace_gemm (0/1: clipvit_gemm_log);
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p"; mx8_skip / mx8_skip_mlp "i,j,.." (bf16
  * blocks; mx8_skip sets both masks). An unknown key or bad value fails with CLIPVIT_E_INVALID
  * and leaves the handle unchanged. The product path never calls it. */
 int clipvit_set_tuning(clipvit_handle* h, const char* spec);
+
+/* Test hook (ABI 4), not part of the reference's surface: with tuning trace_gemm=1, every GEMM
+ * launch of the encoder's Linear roles is logged as 4 ints {role (0 qkv, 1 out_proj, 2 c_fc,
+ * 3 c_proj), tile variant, M, flags (1 blocked W copy, 2 MX-fp8, 4 blocked A, 8 blocked C)}.
+ * Copies up to `cap` entries (4 * cap ints) to out, clears the log and returns the count. */
+int clipvit_gemm_log(clipvit_handle* h, int* out, int cap);
 
 /* Replaces the weight half of clip.load [3p]: host fp32 tensors keyed by OpenAI names.
  * The library copies them to HBM, keeps fp32 masters, and packs the MFMA operands.

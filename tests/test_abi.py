@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.lib().clipvit_abi_version() == 3  # 3: clipvit_set_tuning; the library reads no environment
+    assert _lib.lib().clipvit_abi_version() == 4  # 3: clipvit_set_tuning (no environment reads); 4: clipvit_gemm_log
 
 
 def test_struct_layouts_match_header():

@@ -36,3 +36,19 @@ def test_bench_two_rank_rehearsal(gpu):
     assert d["parity"]["meets_bar"], d["parity"]
     assert d["rccl_world"] == 2 and d["backend"] == "gloo" and d["gather_ok"] is True, d
     assert d["gathered_rows"] == 64
+
+
+def test_bench_self_launch(gpu):
+    """`python bench.py --gpus 2` with no torchrun: bench.py starts the two ranks itself
+    (launch_ranks) and relays rank 0's line, which must report both ranks and a verified gather."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--share-gpu", "--batch", "32",
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--profile-iters", "1"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["ranks"] == 2 and d["rccl_world"] == 2 and d["gather_ok"] is True, d
+    assert d["config"]["global_batch"] == 64 and d["gathered_rows"] == 64
+    assert "launching 2 ranks" in r.stderr

@@ -49,6 +49,9 @@ FLAT_WORST = {("vitb32", "lora"): 1.28e-3, ("vitb32", "lora_new"): 1.42e-3,
               ("vitb16", "lora"): 6.34e-4, ("vitb16", "lora_new"): 5.95e-4}
 FLAT_TOL = max(FLAT_WORST.values()) * 1.1  # the bound for the swap rule's error cap
 GAP_TOL = 1e-4   # fixture probability gap below which two labels may swap
+# the only rank-1 swap outside a fixture tie that the CLIP-scale test admits (ViT-B/16, both
+# checkpoints; fixture logit gap 1.64e-3 against a 2.07e-3 shift from fp16 weight rounding alone)
+B16_RANK1_EXEMPT = {("interior84.jpg", "materials")}
 PROB_TOL = 2e-3
 TEXT_TOL = 2e-3
 CASES = [(m, c) for m in ("vitb32", "vitb16") for c in ("lora", "lora_new")]
@@ -288,8 +291,11 @@ def test_clipscale_harness_meets_north_star_bar(gpu, golden_dir, images, model, 
         # oracle) moves the pair by more than its fixture gap, i.e. no fp16-operand engine can hold
         # it (r05: interior84 'materials', gap 1.6e-3 against a 2.1e-3 weight-rounding shift; the
         # reference's own fp16 CUDA model, emulated, misses this image's logits by 1.4e-2)
+        # The exemption is bounded to that one measured case: the set of
+        # rank-1 swaps must be a subset of it, and each must pass the weight-rounding check below.
         if model == "vitb32":
             assert top1 == 0, (model, ckpt, top1_err)
+        assert {(n, seg) for n, seg, *_ in top1_err} <= B16_RANK1_EXEMPT, (model, ckpt, top1_err)
         for n, seg, la, lb, *_ in top1_err:
             det = seg == "detector"
             flabs = js["detector_categories"] if det else js["categories"][seg]

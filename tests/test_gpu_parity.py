@@ -61,6 +61,11 @@ def _merged(sd, adapters):
 _ENGINES = {}
 
 
+def _fc_tiles(eng):
+    """Tile variants of the c_fc launches logged since the last call (tuning trace_gemm=1)."""
+    return sorted({v for role, v, _, _ in eng.gemm_log() if role == 2})
+
+
 def _engine(cfg, dtype, lora_rank=0, max_batch=256):
     key = (cfg.name, dtype, lora_rank, max_batch)
     if key not in _ENGINES:
@@ -313,9 +318,9 @@ def test_errors_are_reported_not_crashes(gpu):
 
 @pytest.mark.parametrize("dtype", ["fp16", "bf16"])
 def test_full_batch_256_properties(gpu, dtype):
-    """bs=256 (the metric's batch; c_fc on the row split: persistent ping-pong main launch +
-    128x128 tail): every image equals its own bs=1 result bit-for-bit (per-image independence;
-    rows never mix), and a sample of rows matches the oracle."""
+    """bs=256 (the metric's batch; c_fc as ONE balanced launch of variant 75, the fp16 default):
+    every image equals its own bs=1 result bit-for-bit (per-image independence; rows never mix),
+    and a sample of rows matches the oracle."""
     cfg = C.VIT_B32
     eng, ref_sd = _engine(cfg, dtype, 8, max_batch=256)
     px = _pixels(256, 224, seed=3).to(gpu)
@@ -326,10 +331,45 @@ def test_full_batch_256_properties(gpu, dtype):
     for i in (0, 1, 77, 230, 255):
         one = eng.classify(px[i:i + 1]).logits
         assert torch.equal(one[0], full[i]), i
-    idx = [0, 100, 215, 255]  # rows 215.. lie in the c_fc tail launch (rows >= 10752)
+    idx = [0, 100, 215, 255]  # first, middle and last images (v75 tiles of all three rounds)
     f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES["ViT-B/32"], px[idx].cpu())
     _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
     _check_logits(full[idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[(dtype, "peaked")])
+
+
+def test_b32_bs128_round_split_matches_oracle(gpu):
+    """B/32 fp16 bs 128: c_fc's 300 tiles = 1 round + 44, where the whole-round row split is the
+    default (v62 on rows [0, 5376), v81 on the rest). The launch log pins that
+    path; rows of both launches against the oracle at the 1e-3 bar, and the split against the
+    single-launch tile (round_split=0) bit for bit."""
+    cfg = C.VIT_B32
+    sd = synthetic_state_dict(cfg, 0)
+    ad = synthetic_adapters(cfg, rank=8)
+    ref_sd = _merged(sd, ad)
+    px = _pixels(128, 224, seed=45)
+    T = _text(cfg.embed_dim, 437, anchor=_anchor(ref_sd, cfg.name, 224))
+    seg = [0, 40, 60, 359, 395, 425, 437]
+    outs, tiles = {}, {}
+    for split in (1, 0):
+        eng = VisionEngine(cfg, 0, "fp16", max_batch=128, tuning={"trace_gemm": 1, "round_split": split})
+        try:
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            eng.set_text_features(T.numpy(), seg)
+            eng.gemm_log()
+            outs[split] = eng.classify(px.to(gpu)).logits.clone()
+            torch.cuda.synchronize()
+            tiles[split] = _fc_tiles(eng)
+        finally:
+            eng.close()
+    assert tiles[1] == [62, 81], tiles
+    assert tiles[0] == [22], tiles
+    assert torch.equal(outs[0], outs[1])
+    idx = [0, 64, 110, 127]  # 110, 127: rows >= 5376 (image 107.5 on), the v81 launch
+    f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[idx])
+    _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
+    rel = _check_logits(outs[1][idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[("fp16", "peaked")])
+    print(f"B/32 bs 128 (v62 + v81 c_fc): max rel logit err {rel:.2e} on rows {idx}")
 
 
 def test_config4_l14_336_bs128_as_benched(gpu):
@@ -365,12 +405,12 @@ def test_config4_l14_336_bs128_as_benched(gpu):
 
 
 @pytest.mark.parametrize("x24", [1, 0])
-def test_lnfold_bs256_runs_through_the_round_split(gpu, x24):
-    """the LayerNorm-fold path (tuning lnfold=1) at the headline batch, B/32 bs 256,
-    where c_fc's 600 tiles take the whole-round row split. The ping-pong main tiles have only the
-    16-bit STORE / GELU epilogues, so the folded c_fc (EPI_LNF_GELU) must take the single-launch
-    path instead of failing. Rows from the start, middle and end of the batch against the oracle
-    at the 1e-3 bar (peaked text), on the 24-bit residual stream and on fp32 x."""
+def test_lnfold_bs256_takes_the_single_launch(gpu, x24):
+    """the LayerNorm-fold path (tuning lnfold=1) at the headline batch, B/32 bs 256.
+    The balanced v75 launch and the ping-pong round-split tiles have only the 16-bit STORE / GELU
+    epilogues, so the folded c_fc (EPI_LNF_GELU) must take the single-launch v22 tile instead of
+    failing (the launch log pins it). Rows from the start, middle and end of the batch against
+    the oracle at the 1e-3 bar (peaked text), on the 24-bit residual stream and on fp32 x."""
     cfg = C.VIT_B32
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
@@ -378,14 +418,16 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu, x24):
     px = _pixels(256, 224, seed=43)
     T = _text(cfg.embed_dim, 437, anchor=_anchor(ref_sd, cfg.name, 224))
     seg = [0, 40, 60, 359, 395, 425, 437]
-    eng = VisionEngine(cfg, 0, "fp16", max_batch=256, tuning={"lnfold": 1, "x24": x24})
+    eng = VisionEngine(cfg, 0, "fp16", max_batch=256, tuning={"lnfold": 1, "x24": x24, "trace_gemm": 1})
     try:
         eng.load_state_dict(sd)
         eng.load_lora(ad)
         eng.set_text_features(T.numpy(), seg)
+        eng.gemm_log()
         o = eng.classify(px.to(gpu))
         torch.cuda.synchronize()
-        idx = [0, 127, 214, 255]  # 214: a row of c_fc's tail launch (rows >= 10,752 = image 215)
+        assert _fc_tiles(eng) == [22]
+        idx = [0, 127, 214, 255]
         f_ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[idx])
         _, lr, _, _, _ = clip_ref.head(f_ref, T, seg)
         rel = _check_logits(o.logits[idx].cpu().numpy(), lr.numpy(), seg, LOGIT_TOL[("fp16", "peaked")])
@@ -394,68 +436,89 @@ def test_lnfold_bs256_runs_through_the_round_split(gpu, x24):
         eng.close()
 
 
-@pytest.mark.parametrize("name,dtype,B,tun", [
-    ("ViT-B/32", "fp16", 256, {}),              # c_fc: ping-pong v62 main + v81 tail; c_proj v82
-    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),  # the 32-deep-k-step main
-    ("ViT-B/32", "bf16", 67, {}),               # one launch per role
-    ("ViT-B/32", "fp16", 1, {}),                # M = 50: the last 16-row block is padding
-    ("ViT-B/32", "fp16", 256, {"lnfold": 1}),   # EPI_LNF_GELU c_fc, EPI_RES_STATS c_proj
-    ("ViT-B/32", "fp16", 256, {"split_variants": "63,81"}),  # non-temporal ping-pong main
-    ("ViT-B/16", "fp16", 64, {}),               # N = 197, round split
-    ("ViT-L/14@336px", "fp16", 32, {}),         # large M: persistent v63 writes and reads u
-    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3463,80"}),  # v8 direct stores, v80 reads
-    ("ViT-B/32", "mxfp8", 64, {}),              # MX-fp8: fp8 u of the MX blocks, 16-bit u of the rest
-    ("ViT-B/32", "mxfp8", 64, {"mx8_skip": ""}),  # every block MX; the last c_proj keeps u row-major
+# c_fc tile variants each row must reach (the launch log, tuning trace_gemm=1): 75 = the balanced
+# one-launch tile, 62 + 81 / 72 + 81 / 63 + 81 = round split main + tail, 22 = one launch on the
+# 160x128 tile, 74 / 8 = large-M tiles, 3 = the MX-fp8 persistent tile
+@pytest.mark.parametrize("name,dtype,B,tun,fc", [
+    ("ViT-B/32", "fp16", 256, {}, [75]),        # c_fc: one balanced launch (default); c_proj v82
+    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81", "fc_balanced": 0}, [72, 81]),  # 32-deep-k-step main
+    ("ViT-B/32", "fp16", 256, {"fc_balanced": 0}, [62, 81]),  # the round split: ping-pong main + tail
+    ("ViT-B/32", "fp16", 128, {}, [62, 81]),    # bs 128: 1 round + 44 tiles, the round split by default
+    ("ViT-B/32", "bf16", 67, {}, [22]),         # one launch per role
+    ("ViT-B/32", "fp16", 1, {}, [22]),          # M = 50: the last 16-row block is padding
+    ("ViT-B/32", "fp16", 256, {"lnfold": 1}, [22]),  # EPI_LNF_GELU c_fc, EPI_RES_STATS c_proj
+    ("ViT-B/32", "fp16", 256, {"split_variants": "63,81", "fc_balanced": 0}, [63, 81]),  # non-temporal main
+    ("ViT-B/16", "fp16", 64, {}, [75]),         # N = 197: 600 tiles, balanced launch
+    ("ViT-B/16", "fp16", 64, {"fc_balanced": 0}, [62, 81]),  # N = 197, round split
+    ("ViT-L/14@336px", "fp16", 32, {}, [74]),   # large M: persistent v74 writes u, v72 reads it
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3463,80"}, [8]),  # v8 direct stores, v80 reads
+    ("ViT-B/32", "mxfp8", 64, {}, [3, 22]),     # MX-fp8: fp8 u of the MX blocks, 16-bit u of the rest
+    ("ViT-B/32", "mxfp8", 64, {"mx8_skip": ""}, [3]),  # every block MX; the last c_proj keeps u row-major
 ])
-def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun):
+def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun, fc):
     """The c_fc -> c_proj intermediate in the 16-row blocked layout (default; tuning u_blocked=0:
     row-major) moves bytes only: every kernel computes the same values in the same order, so the
-    features equal the row-major run's bit for bit on every GEMM path that writes or reads u."""
+    features equal the row-major run's bit for bit on every GEMM path that writes or reads u.
+    The launch log pins the c_fc tiles each row reaches."""
     cfg = C.get_config(name)
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
     px = _pixels(B, cfg.image_size, seed=47).to(gpu)
     outs = []
     for blk in (1, 0):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, u_blocked=blk))
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, u_blocked=blk, trace_gemm=1))
         try:
             eng.load_state_dict(sd)
             eng.load_lora(ad)
+            eng.gemm_log()
             outs.append(eng.encode_image(px).clone())
             torch.cuda.synchronize()
+            log = eng.gemm_log()
+            assert sorted({v for r, v, _, _ in log if r == 2}) == fc, (tun, log)
+            if blk:  # the blocked u is written by c_fc and read by c_proj on every full-M launch
+                assert any(r == 2 and f & 8 for r, _, _, f in log) and any(r == 3 and f & 4 for r, _, _, f in log)
         finally:
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
 
 
-@pytest.mark.parametrize("name,dtype,B,tun", [
-    ("ViT-B/32", "fp16", 256, {}),                            # QKV v98, out / c_proj v82 read the copy (2); c_fc row-major
-    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81"}),   # c_fc main 72 + tail 81 both read it
-    ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}),          # one launch per role, ragged M
-    ("ViT-B/16", "fp16", 64, {}),                             # N = 197, round split
-    ("ViT-B/16", "fp16", 256, {}),                            # large M: every role on 3472 (default)
-    ("ViT-L/14@336px", "fp16", 32, {}),                       # large M: c_fc on the shipped 3474
-    ("ViT-L/14@336px", "fp16", 64, {}),                       # every role large-M: 3472 / 3474, blocked A
-    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}),  # large-M pipelined tiles
+@pytest.mark.parametrize("name,dtype,B,tun,fc", [
+    ("ViT-B/32", "fp16", 256, {}, [75]),                      # QKV v98, c_fc v75, out / c_proj v82: all read the copy (2)
+    ("ViT-B/32", "fp16", 256, {"split_variants": "72,81", "fc_balanced": 0}, [72, 81]),  # c_fc main 72 + tail 81
+    ("ViT-B/32", "fp16", 256, {"fc_balanced": 0}, [62, 81]),  # the round split (v62 reads the copy, the tail follows it)
+    ("ViT-B/32", "fp16", 128, {}, [62, 81]),                  # bs 128: the round split by default
+    ("ViT-B/32", "bf16", 67, {"qkv_variant": "72"}, [22]),    # one launch per role, ragged M
+    ("ViT-B/16", "fp16", 64, {}, [75]),                       # N = 197, balanced c_fc launch
+    ("ViT-B/16", "fp16", 256, {}, [74]),                      # large M: every role on 3472, c_fc 3474 (default)
+    ("ViT-L/14@336px", "fp16", 32, {}, [74]),                 # large M: c_fc on the shipped 3474
+    ("ViT-L/14@336px", "fp16", 64, {}, [74]),                 # every role large-M: 3472 / 3474, blocked A
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}, [8]),  # large-M pipelined tiles
 ])
-def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun):
-    """QKV / c_fc weights read from their 16-row blocked copy (tuning w_blocked: 1 = the
-    variant-72 launches, the default; 2 = every tile that can) move bytes only: every tile
-    computes the same products in the same order, so the features equal the row-major run's
-    (w_blocked=0) bit for bit — after a LoRA merge, which re-packs both copies."""
+def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun, fc):
+    """The Linear weights read from their 16-row blocked copy (tuning w_blocked: 2 = every tile
+    that can, the default; 1 = the variant-72 / 74 launches only; 0 = none) move bytes only:
+    every tile computes the same products in the same order, so the features equal the
+    row-major run's (w_blocked=0) bit for bit — after a LoRA merge, which re-packs both copies.
+    The launch log pins the c_fc tiles of each row and that w_blocked=0 reads no copy."""
     cfg = C.get_config(name)
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
     px = _pixels(B, cfg.image_size, seed=53).to(gpu)
     outs = []
     for blk in (2, 1, 0):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk))
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk, trace_gemm=1))
         try:
             eng.load_state_dict(sd)
             eng.load_lora(ad)
+            eng.gemm_log()
             outs.append(eng.encode_image(px).clone())
             torch.cuda.synchronize()
+            log = eng.gemm_log()
+            assert sorted({v for r, v, _, _ in log if r == 2}) == fc, (tun, blk, log)
+            copies = sum(1 for _, _, _, f in log if f & 1)
+            want = blk == 2 or (blk == 1 and any(v in (72, 74) for _, v, _, _ in log))
+            assert (copies > 0) == want, (blk, log)
         finally:
             eng.close()
     assert torch.isfinite(outs[0]).all()
