@@ -257,6 +257,7 @@ struct clipvit_handle {
     // c_fc with >= 2 whole rounds of 256x256 tiles plus a remainder: one balanced launch of
     // variant 75 instead of the round split (tuning fc_balanced; gemm() below)
     bool fc_balanced = true;
+    int fc_bal_var = 75;  // its tile: 75 (256 x 256, 200 x 3 at B/32 bs 256) or 77 (320 x 256, 240 x 2); tuning fc_balanced_variant
     // XCD map of the main launch (tile_of_block; tuning split_xcd): 34 = the 1-D remap over a
     // column-group-major order with 2 N-groups, so each XCD group keeps half of W (2.4 MB of
     // c_fc's 4.7) in its 4 MB L2 across its M sweep. Measured: c_fc 0.875-0.879 -> 0.863-0.867
@@ -506,8 +507,8 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             // bits; 69.4 against 71.9 us kernel-level, B/32 +0.7 % same box (3 alternations,
             // profiles/r05/balanced_grid_probe.txt)
             a.xcd_n = h->split_xcd;
-            wsel(a, 75);
-            if (launch(a, 75) == 0) return 0;
+            wsel(a, h->fc_bal_var);
+            if (launch(a, h->fc_bal_var) == 0) return 0;
             wsel(a, 0);
             a.xcd_n = h->xcd[role];
         }
@@ -1165,6 +1166,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "cls_prune") ok = flag(h->cls_prune);
     else if (k == "round_split") ok = flag(h->round_split);
     else if (k == "fc_balanced") ok = flag(h->fc_balanced);
+    else if (k == "fc_balanced_variant") ok = parse_int(v, h->fc_bal_var) && (h->fc_bal_var == 75 || h->fc_bal_var == 77);
     else if (k == "attn_q8") ok = flag(h->attn_q8);
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
@@ -1231,13 +1233,13 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
-        int w_blk, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->w_blk, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1253,7 +1255,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->w_blk = before.w_blk;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1660,7 +1662,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 72 || variant == 74 || variant == 75;
+                        variant == 63 || variant == 72 || variant == 74 || variant == 75 || variant == 77;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

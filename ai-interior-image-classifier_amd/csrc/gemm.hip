@@ -875,14 +875,14 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 / 74 / 75 only
+    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 / 74 / 75 / 77 only
         if (variant < 8 || a.ksplit > 1) return -1;
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
     // blocked W: the pipelined tiles and the persistent tiles (62 / 63 / 72 / 74)
     if (a.blk_w && (variant < 8 || a.ksplit > 1)) return -1;
-    if (variant == 62 || variant == 63 || variant == 72 || variant == 74 || variant == 75)
+    if (variant == 62 || variant == 63 || variant == 72 || variant == 74 || variant == 75 || variant == 77)
         return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

@@ -1,7 +1,7 @@
 // Persistent 256x256 MFMA GEMM with 32-deep k-steps and a four-stage LDS ring (variant 72;
-// round 5). Included by gemm_pp.hip. tools/probes/gemm_p32_diag.h is a copy of this kernel with the
-// diagnostic hooks of profiles/r05_gemm_timeline.md (per-barrier s_memtime stamps, ablations,
-// store policies, AGPR accumulators) for tools/probes/gemm_probe.hip; keep the two in step.
+// round 5). Included by gemm_pp.hip, and by tools/probes/gemm_probe.hip with a diagnostic hook
+// policy (HK: s_memtime stamps at every barrier and inside the read segment, ablations): one
+// source, the library's instantiation (P32NoHooks) compiles every hook to nothing.
 //
 //   C[M, N] = A[M, K] @ W[N, K]^T + bias   (16-bit C; QuickGELU for c_fc)
 //
@@ -46,13 +46,34 @@
 
 namespace clipvit {
 
+// Hook policy of gemm_p32_kernel. The library's: barriers only, no ablation. The probe's policy
+// stamps s_memtime in bar() (arrival / departure), at() (points inside a read segment: 0 after
+// the staging issue, 1 after group 1's counted wait, 2 after the epilogue, 3 after the fragment
+// read issue, 4 after group 1's lgkmcnt(0) drain; in the MFMA segment 5 after its lgkmcnt(0), 6
+// after the MFMA issue) and mark() (around the last epilogue).
+// ABL (diagnostic builds only; their outputs are garbage): 7 no staging, 8 no MFMA, 9 no
+// fragment reads, 3 no epilogue stores.
+struct P32NoHooks {
+    static constexpr int ABL = 0;
+    __device__ __forceinline__ void init(unsigned char*, int, int) {}
+    __device__ __forceinline__ void bar(int, int, int) { __builtin_amdgcn_s_barrier(); }
+    __device__ __forceinline__ void at(int, int, int) {}
+    __device__ __forceinline__ void mark(int, int) {}
+    __device__ __forceinline__ void done() {}
+};
+
 // NT: non-temporal epilogue stores (variant 74: the large-M c_fc, whose u would otherwise sit
 // dirty in the L2 / Infinity Cache in front of the next blocks' operands)
-template <typename T, int EPI, bool BLKA, bool BLKW, int GRP, bool NT>
-__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc) {
+// BM: tile rows, 256 or 320 (variant 77: 320 x 256 tiles, each wave 160 x 64; FM = BM / 32
+// accumulator fragments per column slice, NP = the wave's LDS-DMA pieces per k-step: BM / 64
+// for group 0 (A), 4 for group 1 (W))
+template <typename T, int EPI, bool BLKA, bool BLKW, int GRP, bool NT, int BM, class HK>
+__device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
     typedef typename T::vec8 vec8;
-    constexpr int BM = 256, BN = 256;
-    constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 KB + 16 KB
+    static_assert(BM == 256 || BM == 320, "p32 tile rows");
+    constexpr int BN = 256;
+    constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 / 20 KB + 16 KB
+    constexpr int FM = BM / 32, NP = GRP == 0 ? BM / 64 : 4, HALF = BM / 2;
     constexpr bool GELU = EPI == EPI_GELU;
     // this group's staged operand is in the 16-row blocked layout (blk16_off): the blocked A
     // (c_proj's u) or a blocked weight
@@ -81,11 +102,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         return buf_rsrc(src + (size_t)r0 * ldb, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
     };
     const i32x4_t rs_none = buf_rsrc(src, 0u);  // no next tile: reads return zeros
-    // piece i of this wave = 16 rows 16 p .. 16 p + 15 of the panel, p = 4 wc + i
-    unsigned voff[4];
+    // piece i of this wave = 16 rows 16 p .. 16 p + 15 of the panel, p = NP wc + i
+    unsigned voff[NP];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = 4 * wc + i;
+    for (int i = 0; i < NP; ++i) {
+        const int p = NP * wc + i;
         if constexpr (OWN_BLK) {
             voff[i] = (unsigned)((size_t)p * 16 * ldb + lane * 16);
         } else {
@@ -98,10 +119,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     using T_ = std::true_type;
     using F_ = std::false_type;
     auto stage_pieces = [&](const i32x4_t& r, int kk, int st) {
-        unsigned char* dst = smem + st * STAGE + opbase + 4 * wc * 1024;
+        if constexpr (HK::ABL == 7) return;
+        unsigned char* dst = smem + st * STAGE + opbase + NP * wc * 1024;
         const int so = koff(kk);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) blds16(r, voff[i], so, dst + i * 1024);
+        for (int i = 0; i < NP; ++i) blds16(r, voff[i], so, dst + i * 1024);
     };
 
     int m0, n0, mn = 0, nn = 0;
@@ -112,14 +134,14 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     // fragment addresses: lane (row lrow of a 16-row fragment, k-chunk lg)
     const int lrow = lane & 15, lg = lane >> 4;
     const int swz = ((lg ^ ((lrow >> 2) & 2)) << 4);
-    const int aoff = BLKA ? (GRP * 128 / 16) * 1024 + lg * 256 + lrow * 16 : (GRP * 128 + lrow) * 64 + swz;
+    const int aoff = BLKA ? (GRP * HALF / 16) * 1024 + lg * 256 + lrow * 16 : (GRP * HALF + lrow) * 64 + swz;
     constexpr int AFSTEP = BLKA ? 1024 : 1024;  // 16 rows x 64 B either way
     const int woff = BLKW ? A_ST + (wc * 4) * 1024 + lg * 256 + lrow * 16 : A_ST + (wc * 64 + lrow) * 64 + swz;
-    vec8 af[8], wf[4];
-    f32x4 acc[4][8], bv[4];
+    vec8 af[FM], wf[4];
+    f32x4 acc[4][FM], bv[4];
 
     // fragment reads by inline asm off two base registers per operand (stages 0 / 1, and 2 / 3
-    // 64 KB up) with the stage and fragment offsets as immediates below 40 KB. Plain C++ reads
+    // 2 STAGE up) with the stage and fragment offsets as immediates below 48 KB. Plain C++ reads
     // made hipcc keep one address register per read (ds_read's offset field is 16 bits and the
     // four stages span 128 KB) and spill. The reads are not visible to hipcc's waitcnt pass: every
     // MFMA segment starts with an explicit lgkmcnt(0) (and a sched_barrier, so nothing that uses
@@ -127,14 +149,21 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     unsigned a_lo = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + aoff);
     unsigned w_lo = (unsigned)(size_t)(LDS_AS unsigned char*)(smem + woff);
     unsigned a_hi, w_hi;
-    asm volatile("v_add_u32 %0, 0x10000, %2\n\tv_add_u32 %1, 0x10000, %3"
-                 : "=v"(a_hi), "=v"(w_hi)
-                 : "v"(a_lo), "v"(w_lo));
+    if constexpr (BM == 256) {
+        asm volatile("v_add_u32 %0, 0x10000, %2\n\tv_add_u32 %1, 0x10000, %3"
+                     : "=v"(a_hi), "=v"(w_hi)
+                     : "v"(a_lo), "v"(w_lo));
+    } else {
+        asm volatile("v_add_u32 %0, %4, %2\n\tv_add_u32 %1, %4, %3"
+                     : "=v"(a_hi), "=v"(w_hi)
+                     : "v"(a_lo), "v"(w_lo), "s"(2 * STAGE));
+    }
     auto rd = [&](vec8& d, unsigned base, auto imm) {
         asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(base), "i"(decltype(imm)::value));
     };
     auto reads = [&](auto stc) {
         constexpr int ST = decltype(stc)::value, SO = (ST & 1) * STAGE;
+        if constexpr (HK::ABL == 9) return;
         const unsigned ba = ST >= 2 ? a_hi : a_lo, bw = ST >= 2 ? w_hi : w_lo;
         rd(wf[0], bw, std::integral_constant<int, SO>{});
         rd(wf[1], bw, std::integral_constant<int, SO + 1024>{});
@@ -148,21 +177,27 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         rd(af[5], ba, std::integral_constant<int, SO + 5 * AFSTEP>{});
         rd(af[6], ba, std::integral_constant<int, SO + 6 * AFSTEP>{});
         rd(af[7], ba, std::integral_constant<int, SO + 7 * AFSTEP>{});
+        if constexpr (FM > 8) {
+            rd(af[8 % FM], ba, std::integral_constant<int, SO + 8 * AFSTEP>{});
+            rd(af[9 % FM], ba, std::integral_constant<int, SO + 9 * AFSTEP>{});
+        }
     };
     auto mfmas = [&](auto first) {
         constexpr bool FIRST = decltype(first)::value;
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int fm = 0; fm < 8; ++fm)
+        for (int fm = 0; fm < FM; ++fm)
 #pragma unroll
             for (int fn = 0; fn < 4; ++fn) {
-                acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fn][fm]);
+                if constexpr (HK::ABL == 8) asm volatile("" ::"v"(wf[fn]), "v"(af[fm]));
+                else acc[fn][fm] = T::mfma16(wf[fn], af[fm], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[fn][fm]);
             }
         __builtin_amdgcn_s_setprio(0);
     };
-    auto bar = [&] {
+    int ti = 0;  // tiles finished by this workgroup (hook policy only)
+    auto bar = [&](int step, int seg) {
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
+        hk.bar(ti, step, seg);
         __builtin_amdgcn_sched_barrier(0);
     };
     // the tile's bias vector slice (16 features per lane) from LDS: inline asm with its own wait
@@ -185,8 +220,8 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         const int n = pn0 + wc * 64 + 16 * (le >> 4);
         load_bias(pn0);  // the finished tile's bias slice
 #pragma unroll
-        for (int fm = 0; fm < 8; ++fm) {
-            const int m = pm0 + GRP * 128 + fm * 16 + (le & 15);
+        for (int fm = 0; fm < FM; ++fm) {
+            const int m = pm0 + GRP * HALF + fm * 16 + (le & 15);
             float v[16];
 #pragma unroll
             for (int f = 0; f < 4; ++f)
@@ -220,7 +255,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                 off = ((size_t)m * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
                 off2 = off + 64;
             }
-            if (m < a.M) {
+            if (m < a.M && (HK::ABL != 3 || a.ldc < 0)) {
                 if constexpr (NT) {
                     __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
                     __builtin_nontemporal_store(w1, (u32x4*)(Cb + off2));
@@ -233,10 +268,12 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         }
     };
 
-    // vmcnt allowances: 8 = the two younger issue groups of 4 pieces; 24 when the previous
-    // tile's 16 epilogue stores are also younger than the awaited pieces. On a workgroup's first
-    // tile there is no previous tile: 16 stores through a zero-length buffer resource (dropped by
-    // the range check) take the epilogue's place, so the counts and the code are the same.
+    // vmcnt allowances: W_LO = the two younger issue groups of NP pieces (8 at BM = 256);
+    // W_HI (24) when the previous tile's 2 FM epilogue stores are also younger than the awaited
+    // pieces. On a workgroup's first tile there is no previous tile: 2 FM stores through a
+    // zero-length buffer resource (dropped by the range check) take the epilogue's place, so the
+    // counts and the code are the same.
+    constexpr int W_LO = 2 * NP, W_HI = 2 * NP + 2 * FM;
     const i32x4_t rs_drop = buf_rsrc(a.C, 0u);
     auto null_stores = [&]() {  // inline asm: hipcc would merge 16 identical stores into one
         const u32x4 z = {0u, 0u, 0u, 0u};
@@ -252,13 +289,21 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             :
             : "v"(z), "s"(rs_drop)
             : "memory");
+        if constexpr (FM > 8) {
+            asm volatile(
+                "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+                "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0"
+                :
+                : "v"(z), "s"(rs_drop)
+                : "memory");
+        }
     };
     //
     // one k-step (compile-time position): ST / STI = stage read / staged; NXT = the staged step
     // belongs to the next tile (kk = step within that tile); FIRST = the tile's first step (its
     // MFMAs start the accumulators from 0; the bias is added in the epilogue); EP = it carries the
     // previous tile's epilogue; W24 =
-    // wait allowance 24 instead of 8
+    // wait allowance W_HI instead of W_LO
     auto kstep = [&](int step, int kk_issue, auto nxt, auto stc, auto stic, auto first, auto ep, auto w24,
                      bool have_prev, int pm0, int pn0) {
         constexpr bool EP = decltype(ep)::value;
@@ -267,25 +312,34 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         // counted wait, the previous tile's epilogue (its stores younger than every piece the
         // next waits count), the tile's bias slice, the fragment reads ----
         stage_pieces(decltype(nxt)::value ? rs_n : rs_c, kk_issue, decltype(stic)::value);
+        hk.at(ti, step, 0);
         if constexpr (GRP == 1) {  // pieces of step t + 1 (issued two read segments ago) landed
-            if (W24) vm_wait<24>(); else vm_wait<8>();
+            if (W24) vm_wait<W_HI>(); else vm_wait<W_LO>();
+            hk.at(ti, step, 1);
         }
         if constexpr (EP) {
             if (have_prev) epilogue(pm0, pn0);
             else null_stores();
+            hk.at(ti, step, 2);
         }
         reads(stc);
-        if constexpr (GRP == 1) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
-        bar();
+        hk.at(ti, step, 3);
+        if constexpr (GRP == 1) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): WAR of the stage
+            hk.at(ti, step, 4);
+        }
+        bar(step, 0);
         // ---- MFMA segment ----
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the fragment reads (inline asm) landed
+        hk.at(ti, step, 5);
         __builtin_amdgcn_sched_barrier(0);
         mfmas(first);
         __builtin_amdgcn_sched_barrier(0);
+        hk.at(ti, step, 6);
         if constexpr (GRP == 0) {
-            if (W24) vm_wait<24>(); else vm_wait<8>();
+            if (W24) vm_wait<W_HI>(); else vm_wait<W_LO>();
         }
-        bar();
+        bar(step, 1);
     };
     // prologue: steps 0, 1, 2 of the first tile; the bias vector of the whole GEMM -> LDS
     stage_pieces(rs_c, 0, 0);
@@ -308,7 +362,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
     for (int f = 0; f < 4; ++f)
 #pragma unroll
-        for (int m = 0; m < 8; ++m) acc[f][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int m = 0; m < FM; ++m) acc[f][m] = f32x4{0.f, 0.f, 0.f, 0.f};
     int pm0 = 0, pn0 = 0;
     for (int i = 1;; ++i) {
         const bool have_prev = i > 1;
@@ -331,6 +385,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         kstep(nk - 1, 2, T_{}, S3{}, S2{}, F_{}, F_{}, F_{}, false, 0, 0);
         pm0 = m0;
         pn0 = n0;
+        ++ti;
         if (!has_next) break;
         m0 = mn;
         n0 = nn;
@@ -338,18 +393,25 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         has_next = tile(i + 1, mn, nn);
         rs_n = has_next ? rsrc_of(mn, nn) : rs_none;
     }
+    hk.mark(ti, 0);
     epilogue(pm0, pn0);
+    hk.mark(ti, 1);
     if constexpr (GRP == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
     vm_wait<0>();
 }
 
-template <typename T, int EPI, bool BLKA, bool BLKW = false, bool NT = false>
+// LDS: four stages of (BM + 256) x 64 B, then the GEMM's bias vector (fp32): 160 KB in all, so
+// N <= 8192 at BM = 256 and N <= 4096 at BM = 320 (launch_p32_t checks)
+template <typename T, int EPI, bool BLKA, bool BLKW = false, bool NT = false, int BM = 256, class HK = P32NoHooks>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, 0, NT>(a, ntiles, smem, lane, wave);
-    else p32_body<T, EPI, BLKA, BLKW, 1, NT>(a, ntiles, smem, lane, wave - 4);
+    HK hk;
+    hk.init(smem, lane, wave);
+    if (wave < 4) p32_body<T, EPI, BLKA, BLKW, 0, NT, BM, HK>(a, ntiles, smem, lane, wave, hk);
+    else p32_body<T, EPI, BLKA, BLKW, 1, NT, BM, HK>(a, ntiles, smem, lane, wave - 4, hk);
+    hk.done();
 }
 
 }  // namespace clipvit

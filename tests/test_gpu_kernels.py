@@ -31,13 +31,14 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # The shipped tiles: 1-3 shape fallback, 8 / 80 256x256, 81 128x128, 22 / 82 160x128,
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 62 the persistent 256x256 ping-pong tile
 # (gemm_pp.hip; 63 the same with non-temporal stores; 72 the 32-deep-k-step persistent tile of
-# gemm_p32.h; 74 the same with non-temporal stores); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
+# gemm_p32.h; 74 the same with non-temporal stores; 75 on a balanced grid; 77 its 320 x 256 form on a balanced
+# grid); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 74, 75, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472, 3474, 3480,
-            10008, 10022, 10062, 10063, 10072, 10080, 10081, 10082, 10090, 10098, 13462, 13472]
+VARIANTS = [1, 2, 3, 8, 22, 62, 63, 72, 74, 75, 77, 80, 81, 82, 90, 98, 208, 222, 280, 282, 298, 3408, 3462, 3463, 3472,
+            3474, 3477, 3480, 10008, 10022, 10062, 10063, 10072, 10077, 10080, 10081, 10082, 10090, 10098, 13462, 13472, 13477]
 N128 = (1, 2, 22, 81, 82)
-N256 = (3, 8, 62, 63, 72, 74, 75, 80, 98)
-STAGED = (62, 63, 72, 74, 75, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 62, 63, 72, 74, 75, 77, 80, 98)
+STAGED = (62, 63, 72, 74, 75, 77, 80, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -54,7 +55,7 @@ def _skip(variant, N, K):
         return "tile does not divide N"
     if v in (62, 63) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
-    if v in (72, 74, 75) and (K % 128 or K < 256):
+    if v in (72, 74, 75, 77) and (K % 128 or K < 256):
         return "32-deep-k-step tile: K a multiple of 128, >= 256"
     return None
 
@@ -77,7 +78,7 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("variant", STAGED + (8, 22, 10072, 10081, 10098))
+@pytest.mark.parametrize("variant", STAGED + (8, 22, 10072, 10077, 10081, 10098))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous
@@ -241,7 +242,7 @@ def test_ping_pong_race_screen(gpu, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
                                    (36928 // 4, 4096, 1024), (50432, 2304, 768)])
 def test_p32_race_screen(gpu, M, N, K):
-    """The 32-deep-k-step persistent tiles (72 / 74 non-temporal / 75 on the balanced grid; the large-M roles' and the B/32
+    """The 32-deep-k-step persistent tiles (72 / 74 non-temporal / 75 on the balanced grid / 77 its 320 x 256 form; the large-M roles' and the B/32
     c_fc main launch's default since r05, with the blocked weight copy: + 10000) hand their four
     LDS stages between the two wave groups by counted vmcnt and barriers only. Their arithmetic is
     v8's (accumulate from 0, then + bias, QuickGELU), so the outputs must equal v8's bit for bit
@@ -254,7 +255,7 @@ def test_p32_race_screen(gpu, M, N, K):
     bias = torch.randn(N, device=gpu, generator=g)
     for epi in (10, 11):  # 16-bit store / QuickGELU
         ref = E.gemm_test(A, W, bias, epi=epi, variant=8)
-        for variant in (72, 3472, 10072, 13472, 74, 13474, 10075):
+        for variant in (72, 3472, 10072, 13472, 74, 13474, 10075, 77, 3477, 10077, 13477):
             for _ in range(4):
                 C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())

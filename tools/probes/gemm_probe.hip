@@ -1,16 +1,18 @@
-// GEMM timeline probe (diagnostic build, never shipped): the persistent ping-pong tile of
-// csrc/gemm_pp.hip (variant 62) with
-//   * in-kernel stamps: s_memtime at every barrier of the first 12 k-tiles of each workgroup's
-//     first three tiles, around the epilogue, and s_memtime / s_memrealtime at kernel start and
-//     end (the in-kernel clock, MI355X_MICROARCH.md "DVFS give-back" item 6). Stamps go to the
-//     unused part of the bias area of LDS by inline-asm ds_write (invisible to the waitcnt pass,
-//     so the counted vmcnt of the staging pipeline is untouched) and to a trace buffer at exit;
-//   * the ablations that used to live in the shipped source (CLIPVIT_ABLATE): 3 no epilogue
-//     stores, 7 no staging after the first two k-tiles, 8 no MFMA.
+// GEMM timeline probe (diagnostic build, never shipped):
+//   * p32 / p32run: the SHIPPED 32-deep-k-step kernel (csrc/gemm_p32.h, included as is) with the
+//     stamp policy P32Stamp (s_memtime at every barrier and at the read / MFMA segments' inner
+//     points, in-kernel clock from s_memtime / s_memrealtime) or an ablation policy P32Abl<N>
+//     (7 no staging, 8 no MFMA, 9 no fragment reads, 3 no epilogue stores): the per-phase cycle
+//     table of profiles/r06_gemm_phases.md, and plain launches for PMC passes;
+//   * the persistent ping-pong tile of csrc/gemm_pp.hip (variant 62) as a stamped copy
+//     (ppp_probe), with s_memtime at every barrier of the first 12 k-tiles of a workgroup's first
+//     three tiles; stamps go to the unused part of the bias area of LDS by inline-asm ds_write
+//     (invisible to the waitcnt pass, so the counted vmcnt of the staging pipeline is untouched);
+//   * bar: barrier / MFMA-segment micro-probes.
 //
 // hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm --amdgpu-mfma-vgpr-form \
 //       -o tools/probes/gemm_probe tools/probes/gemm_probe.hip
-// ./gemm_probe M N K epi xcd [iters] [grid]      (epi 0 store, 1 QuickGELU)
+// ./gemm_probe p32 M N K epi xcd [balanced] | p32run M N K epi xcd iters kind | bar | M N K epi xcd [iters] [grid]
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -19,7 +21,7 @@
 #include <vector>
 
 #include "../../ai-interior-image-classifier_amd/csrc/common.h"
-#include "gemm_p32_diag.h"
+#include "../../ai-interior-image-classifier_amd/csrc/gemm_p32.h"  // the shipped kernel, with a hook policy below
 
 using namespace clipvit;
 
@@ -329,53 +331,68 @@ __global__ __launch_bounds__(512, 1) void ppp_probe(GemmArgs a, int ntiles, unsi
 }
 
 
-// ---- stamped barrier policy for variant 72 (gemm_p32.h): s_memtime on arrival at and departure
-// from every barrier of the first 3 tiles (24 k-steps each), and around the epilogue ----
-constexpr int P32_TILE = 24 * 5 + 4;  // per tile: [step][seg][arrive, depart], marks, [step] after-issue
+// ---- hook policies for variant 72 (gemm_p32.h's HK parameter) ----
+// Stamps: s_memtime (+ lgkmcnt(0), so a stamp never reads a pending SGPR) written by lane 0 into the
+// unused part of the bias area of LDS by inline-asm ds_write (invisible to the waitcnt pass: the
+// counted vmcnt of the staging pipeline is untouched), copied to g_p32_trace at exit. Per k-step of
+// the first two tiles: the four barrier stamps (arrival / departure of the read and MFMA
+// segments' closing barriers) and the at() points: 0 after the staging issue, 1 after group 1's
+// counted vm wait, 2 after the epilogue, 3 after the fragment reads (group 1 only; the stamp's
+// own lgkmcnt(0) drains them, which group 1 does next anyway), 5 after the MFMA segment's
+// lgkmcnt(0), 6 after the MFMA issue (group 0's vm wait follows).
+constexpr int P32_STEP = 10, P32_TILE = 24 * P32_STEP;
 __device__ unsigned* g_p32_trace;
+template <int AB = 0>
+struct P32Abl {  // ablation only, no stamps
+    static constexpr int ABL = AB;
+    __device__ __forceinline__ void init(unsigned char*, int, int) {}
+    __device__ __forceinline__ void bar(int, int, int) { __builtin_amdgcn_s_barrier(); }
+    __device__ __forceinline__ void at(int, int, int) {}
+    __device__ __forceinline__ void mark(int, int) {}
+    __device__ __forceinline__ void done() {}
+};
 struct P32Stamp {
+    static constexpr int ABL = 0;
     unsigned* sbuf;
     int lane, wave;
     unsigned long long m0, r0;
     __device__ void init(unsigned char* smem, int l, int w) {
-        sbuf = (unsigned*)(smem + 4 * 512 * 64) + 4096 + w * NST;
+        sbuf = (unsigned*)(smem + 4 * 512 * 64) + 4096 + w * NST;  // N <= 4096
         lane = l;
         wave = w;
         m0 = __builtin_amdgcn_s_memtime();
         r0 = __builtin_amdgcn_s_memrealtime();
     }
     __device__ void put(int idx, unsigned v) {
-        if (lane == 0) {
+        if (lane == 0 && idx < NST) {
             const unsigned a = (unsigned)(size_t)(LDS_AS unsigned*)(sbuf + idx);
             asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
         }
     }
     __device__ void bar(int ti, int step, int seg) {
-        if (ti < 3 && step < 24) {
+        if (ti < 2 && step < 24) {
             unsigned long long ta, td;
             asm volatile("s_memtime %0\n\ts_barrier\n\ts_memtime %1\n\ts_waitcnt lgkmcnt(0)" : "=&s"(ta), "=&s"(td)::"memory");
-            const int i = 8 + ti * P32_TILE + step * 4 + seg * 2;
+            const int i = 8 + ti * P32_TILE + step * P32_STEP + seg * 2;
             put(i, (unsigned)ta);
             put(i + 1, (unsigned)td);
         } else {
             __builtin_amdgcn_s_barrier();
         }
     }
-    __device__ void sub(int ti, int step) {
-        if (ti < 3 && step < 24) {
+    __device__ void at(int ti, int step, int pt) {
+        if (ti < 2 && step < 24 && pt != 4) {
             unsigned long long t;
             asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            put(8 + ti * P32_TILE + 100 + step, (unsigned)t);
+            put(8 + ti * P32_TILE + step * P32_STEP + 4 + (pt > 4 ? pt - 1 : pt), (unsigned)t);
         }
     }
     __device__ void mark(int ti, int which) {
-        if (ti < 4 && ti >= 1) {
-            unsigned long long t;
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            put(8 + (ti - 1) * P32_TILE + 96 + which, (unsigned)t);
-        }
+        unsigned long long t;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        put(8 + 2 * P32_TILE + which, (unsigned)t);
     }
-    __device__ void done(const GemmArgs&) {
+    __device__ void done() {
         const unsigned long long m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
         __syncthreads();
         unsigned* out = g_p32_trace + ((size_t)blockIdx.x * 8 + wave) * NST;
@@ -623,9 +640,12 @@ int main(int argc, char** argv) {
         seg_case<16, 2, 12, 3>(src, 2000);
         return 0;
     }
-    if (argc > 1 && std::string(argv[1]) == "p32run") {  // p32run M N K epi xcd iters kind (PMC passes)
+    // p32run M N K epi xcd iters kind: plain launches for PMC passes. kind 0 v72 row-major A / W,
+    // 1 v72 blocked A + W, 2 the v62 copy, 3 the shipped c_fc (v75: row-major A, blocked W,
+    // balanced grid)
+    if (argc > 1 && std::string(argv[1]) == "p32run") {
         const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), epi = atoi(argv[5]), xcd = atoi(argv[6]);
-        const int iters = atoi(argv[7]), kind = argc > 8 ? atoi(argv[8]) : 0;  // 0 v72, 1 v72 blocked A + W, 2 v62
+        const int iters = atoi(argv[7]), kind = argc > 8 ? atoi(argv[8]) : 0;
         u16 *A, *W, *C;
         float* bias;
         CK(hipMalloc(&A, (size_t)(M + 256) * K * 2));
@@ -638,7 +658,8 @@ int main(int argc, char** argv) {
         GemmArgs a{};
         a.A = A; a.W = W; a.bias = bias; a.C = C;
         a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd;
-        const int ntiles = ((M + 255) / 256) * (N / 256), grid = std::min(ntiles, 256);
+        const int ntiles = ((M + 255) / 256) * (N / 256), per = (ntiles + 255) / 256;
+        const int grid = kind == 3 ? (ntiles + per - 1) / per : std::min(ntiles, 256);
         for (int i = 0; i < iters; ++i) {
             if (kind == 2) {
                 if (epi) ppp_probe<F16, EPI_GELU, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
@@ -646,6 +667,9 @@ int main(int argc, char** argv) {
             } else if (kind == 1) {
                 if (epi) gemm_p32_kernel<F16, EPI_GELU, true, true><<<grid, 512>>>(a, ntiles);
                 else gemm_p32_kernel<F16, EPI_STORE, true, true><<<grid, 512>>>(a, ntiles);
+            } else if (kind == 3) {
+                if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true><<<grid, 512>>>(a, ntiles);
+                else gemm_p32_kernel<F16, EPI_STORE, false, true><<<grid, 512>>>(a, ntiles);
             } else {
                 if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles);
                 else gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles);
@@ -655,8 +679,12 @@ int main(int argc, char** argv) {
         printf("p32run done\n");
         return 0;
     }
-    if (argc > 1 && std::string(argv[1]) == "p32") {  // p32 M N K epi xcd: operand layout experiment
+    // p32 M N K epi xcd [balanced]: the shipped kernel (row-major A, blocked W, as c_fc / QKV run
+    // it) with the stamp policy after ~2 s of plain launches: the per-phase cycle table of the
+    // k-loop; then the ablations (P32Abl) and the plain kernel, best of 5 x 20 launches.
+    if (argc > 1 && std::string(argv[1]) == "p32") {
         const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), epi = atoi(argv[5]), xcd = atoi(argv[6]);
+        const bool bal = argc > 7 && atoi(argv[7]) != 0;
         u16 *A, *W, *C;
         float* bias;
         CK(hipMalloc(&A, (size_t)(M + 256) * K * 2));
@@ -668,8 +696,10 @@ int main(int argc, char** argv) {
         CK(hipMemset(bias, 0, N * 4));
         GemmArgs a{};
         a.A = A; a.W = W; a.bias = bias; a.C = C;
-        a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd;
-        const int ntiles = ((M + 255) / 256) * (N / 256), grid = std::min(ntiles, 256);
+        a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd; a.blk_w = 1;
+        const int ntiles = ((M + 255) / 256) * (N / 256), per = (ntiles + 255) / 256;
+        const int grid = bal ? (ntiles + per - 1) / per : std::min(ntiles, 256);
+        printf("p32 %dx%dx%d epi%d xcd%d: %d tiles on %d workgroups\n", M, N, K, epi, xcd, ntiles, grid);
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
@@ -685,9 +715,8 @@ int main(int argc, char** argv) {
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 best = std::min(best, ms / 20);
             }
-            printf("%-40s %7.2f us  %.0f TF/s\n", name, best * 1e3, 2.0 * M * N * K / (best * 1e-3) / 1e12);
+            printf("%-34s %7.2f us  %.0f TF/s\n", name, best * 1e3, 2.0 * M * N * K / (best * 1e-3) / 1e12);
         };
-        // stamped run of the default layout after 2 s of plain launches
         {
             unsigned* tr;
             CK(hipMalloc(&tr, (size_t)grid * 8 * NST * 4));
@@ -697,110 +726,81 @@ int main(int argc, char** argv) {
             float ms = 0.f;
             while (ms < 2000.f) {
                 for (int i = 0; i < 100; ++i) {
-                    if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles);
-                    else gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles);
+                    if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true><<<grid, 512>>>(a, ntiles);
+                    else gemm_p32_kernel<F16, EPI_STORE, false, true><<<grid, 512>>>(a, ntiles);
                 }
                 CK(hipEventRecord(e1));
                 CK(hipEventSynchronize(e1));
                 CK(hipEventElapsedTime(&ms, e0, e1));
             }
-            if (epi) gemm_p32_kernel<F16, EPI_GELU, false, false, 0, P32Stamp><<<grid, 512>>>(a, ntiles);
-            else gemm_p32_kernel<F16, EPI_STORE, false, false, 0, P32Stamp><<<grid, 512>>>(a, ntiles);
+            if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, false, 256, P32Stamp><<<grid, 512>>>(a, ntiles);
+            else gemm_p32_kernel<F16, EPI_STORE, false, true, false, 256, P32Stamp><<<grid, 512>>>(a, ntiles);
             CK(hipDeviceSynchronize());
             std::vector<unsigned> t((size_t)grid * 8 * NST);
             CK(hipMemcpy(t.data(), tr, t.size() * 4, hipMemcpyDeviceToHost));
             auto u64 = [&](const unsigned* p, int i) { return (unsigned long long)p[i] | ((unsigned long long)p[i + 1] << 32); };
-            auto med = [](std::vector<double>& v) { std::sort(v.begin(), v.end()); return v.empty() ? -1.0 : v[v.size() / 2]; };
+            auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? -1.0 : v[v.size() / 2]; };
             std::vector<double> clk, span;
             for (int g = 0; g < grid; ++g) {
                 const unsigned* p = &t[(size_t)g * 8 * NST];
                 clk.push_back((double)(u64(p, 4) - u64(p, 0)) / (double)(u64(p, 6) - u64(p, 2)) * 0.1);
                 span.push_back((double)(u64(p, 6) - u64(p, 2)) * 0.01);
             }
-            printf("stamped p32: in-kernel clock %.3f GHz (median), workgroup span %.2f us (median)\n", med(clk), med(span));
+            printf("stamped: in-kernel clock %.3f GHz (median), workgroup span %.2f us (median)\n", med(clk), med(span));
             const int nks = std::min(K / 32, 24);
+            // slot of a stamp: [0] arrive R-barrier, [1] depart, [2] arrive M-barrier, [3] depart,
+            // [4 + p] at() point p (0 issue, 1 vm wait, 2 epilogue, 3 reads, 4 -> 5 M lgkm, 5 -> 6 MFMA issue)
+            auto slot = [&](int tix, int st, int k) { return 8 + tix * P32_TILE + st * P32_STEP + k; };
+            // a phase = median over workgroups of stamp(b) - stamp(a) for one wave
+            auto phase = [&](int wv, int tix, int st, int sa, int ka, int sb, int kb) {
+                std::vector<double> v;
+                for (int g = 0; g < grid; ++g) {
+                    const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
+                    const unsigned x = p[slot(tix, sa, ka)], y = p[slot(tix, sb, kb)];
+                    if (x && y) v.push_back((double)(unsigned)(y - x));
+                }
+                return med(v);
+            };
+            const char* names[] = {"R: staging issue", "R: vm wait (group 1)", "R: frag reads issue+drain / issue",
+                                   "R: to barrier", "R: barrier wait", "M: lgkm drain", "M: MFMA issue",
+                                   "M: vm wait (group 0) + to barrier", "M: barrier wait", "k-step"};
             for (int tix = 0; tix < 2; ++tix)
                 for (int wv : {0, 4}) {
-                    printf("tile %d wave %d: per k-step [read seg work/wait | MFMA seg work/wait] cycles\n", tix, wv);
-                    double sr = 0, sm = 0, sx = 0;
+                    const bool g1 = wv >= 4;
+                    double acc[10] = {0};
                     int nn = 0;
-                    for (int st = 0; st < nks; ++st) {
-                        double v4[4];
-                        for (int seg = 0; seg < 2; ++seg) {
-                            std::vector<double> w, x;
-                            for (int g = 0; g < grid; ++g) {
-                                const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
-                                const int i = 8 + tix * P32_TILE + st * 4 + seg * 2;
-                                const int dprev = seg == 1 ? i - 1 : (st > 0 ? i - 3 : -1);
-                                if (!p[i] || !p[i + 1]) continue;
-                                x.push_back((double)(unsigned)(p[i + 1] - p[i]));
-                                if (dprev >= 0 && p[dprev]) w.push_back((double)(unsigned)(p[i] - p[dprev]));
-                            }
-                            v4[2 * seg] = med(w);
-                            v4[2 * seg + 1] = med(x);
-                        }
-                        std::vector<double> is;
-                        for (int g = 0; g < grid; ++g) {
-                            const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
-                            const int i = 8 + tix * P32_TILE + st * 4;
-                            const unsigned su = p[8 + tix * P32_TILE + 100 + st];
-                            if (st > 0 && su && p[i - 1]) is.push_back((double)(unsigned)(su - p[i - 1]));
-                        }
-                        const double iss = med(is);
-                        if (st < 4 || st >= nks - 2 || st == nks / 2)
-                            printf("  step %2d: R %5.0f/%-5.0f (staging issue %5.0f) | M %5.0f/%-5.0f\n", st, v4[0], v4[1], iss, v4[2], v4[3]);
-                        if (st >= 4 && st < nks - 1) { sr += v4[0]; sm += v4[2]; sx += v4[1] + v4[3]; ++nn; }
+                    for (int st = 4; st < nks - 1; ++st) {
+                        double ph[10];
+                        ph[0] = phase(wv, tix, st - 1, st - 1, 3, st, 4);          // depart M(t-1) -> issue
+                        ph[1] = g1 ? phase(wv, tix, st, st, 4, st, 5) : 0.0;      // issue -> vm wait
+                        ph[2] = g1 ? phase(wv, tix, st, st, 5, st, 7) : phase(wv, tix, st, st, 4, st, 0);  // reads
+                        ph[3] = g1 ? phase(wv, tix, st, st, 7, st, 0) : 0.0;
+                        ph[4] = phase(wv, tix, st, st, 0, st, 1);
+                        ph[5] = phase(wv, tix, st, st, 1, st, 8);
+                        ph[6] = phase(wv, tix, st, st, 8, st, 9);
+                        ph[7] = phase(wv, tix, st, st, 9, st, 2);
+                        ph[8] = phase(wv, tix, st, st, 2, st, 3);
+                        ph[9] = phase(wv, tix, st - 1, st - 1, 3, st, 3);
+                        for (int k = 0; k < 10; ++k) acc[k] += ph[k];
+                        ++nn;
                     }
-                    if (nn) printf("  steady (steps 4..%d): R work %.0f + M work %.0f + waits %.0f = %.0f cyc per k-step\n", nks - 2, sr / nn, sm / nn, sx / nn, (sr + sm + sx) / nn);
-                    std::vector<double> ep;
-                    for (int g = 0; g < grid; ++g) {
-                        const unsigned* p = &t[((size_t)g * 8 + wv) * NST];
-                        const int i = 8 + tix * P32_TILE + 96;
-                        if (p[i] && p[i + 1]) ep.push_back((double)(unsigned)(p[i + 1] - p[i]));
-                    }
-                    printf("  epilogue of this tile (in the next tile's first read segment): %.0f cyc (n=%zu)\n", med(ep), ep.size());
+                    printf("tile %d wave %d (group %d), steady steps 4..%d, cycles per k-step (median over WGs):\n", tix, wv, g1, nks - 2);
+                    for (int k = 0; k < 10; ++k) printf("  %-36s %6.0f\n", names[k], acc[k] / nn);
                 }
             CK(hipFree(tr));
         }
         for (int rep = 0; rep < 2; ++rep) {
-            if (epi) {
-                run("p32 A row-major, W row-major", [&] { gemm_p32_kernel<F16, EPI_GELU, false, false><<<grid, 512>>>(a, ntiles); });
-                run("p32 A blocked,   W row-major", [&] { gemm_p32_kernel<F16, EPI_GELU, true, false><<<grid, 512>>>(a, ntiles); });
-                run("p32 A row-major, W blocked", [&] { gemm_p32_kernel<F16, EPI_GELU, false, true><<<grid, 512>>>(a, ntiles); });
-                run("p32 A blocked,   W blocked", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true><<<grid, 512>>>(a, ntiles); });
-            } else {
-                run("p32 A row-major, W row-major", [&] { gemm_p32_kernel<F16, EPI_STORE, false, false><<<grid, 512>>>(a, ntiles); });
-                run("p32 A blocked,   W row-major", [&] { gemm_p32_kernel<F16, EPI_STORE, true, false><<<grid, 512>>>(a, ntiles); });
-                run("p32 A row-major, W blocked", [&] { gemm_p32_kernel<F16, EPI_STORE, false, true><<<grid, 512>>>(a, ntiles); });
-                run("p32 A blocked,   W blocked", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true><<<grid, 512>>>(a, ntiles); });
-            }
-            if (epi) {
-                run("p32 blocked: no staging", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 7><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no MFMA", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 8><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no fragment reads", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 9><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no stores", [&] { gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 3><<<grid, 512>>>(a, ntiles); });
-            } else {
-                run("p32 blocked: no staging", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 7><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no MFMA", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 8><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no fragment reads", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 9><<<grid, 512>>>(a, ntiles); });
-                run("p32 blocked: no stores", [&] { gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 3><<<grid, 512>>>(a, ntiles); });
-            }
-            run("p32 W blocked, AGPR accumulators", [&] {
-                if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
-                else gemm_p32_kernel<F16, EPI_STORE, false, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
-            });
-            run("p32 A + W blocked, AGPR accumulators", [&] {
-                if (epi) gemm_p32_kernel<F16, EPI_GELU, true, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
-                else gemm_p32_kernel<F16, EPI_STORE, true, true, 0, P32Barrier, false, 0, false, 0, true><<<grid, 512>>>(a, ntiles);
-            });
-            run("p32 W blocked: stores into 256 rows", [&] {
-                if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, 0, P32Barrier, false, 0, false, 4><<<grid, 512>>>(a, ntiles);
-                else gemm_p32_kernel<F16, EPI_STORE, false, true, 0, P32Barrier, false, 0, false, 4><<<grid, 512>>>(a, ntiles);
-            });
-            run("v62 copy (ppp_probe)", [&] {
-                if (epi) ppp_probe<F16, EPI_GELU, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
-                else ppp_probe<F16, EPI_STORE, 0, false><<<grid, 512>>>(a, ntiles, nullptr);
-            });
+#define P32RUN(NAME, HKT)                                                                          \
+    run(NAME, [&] {                                                                                \
+        if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, false, 256, HKT><<<grid, 512>>>(a, ntiles); \
+        else gemm_p32_kernel<F16, EPI_STORE, false, true, false, 256, HKT><<<grid, 512>>>(a, ntiles);    \
+    })
+            P32RUN("shipped (A row-major, W blocked)", P32Abl<0>);
+            P32RUN("ablation: no staging", P32Abl<7>);
+            P32RUN("ablation: no MFMA", P32Abl<8>);
+            P32RUN("ablation: no fragment reads", P32Abl<9>);
+            P32RUN("ablation: no epilogue stores", P32Abl<3>);
+#undef P32RUN
         }
         return 0;
     }

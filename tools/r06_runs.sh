@@ -38,11 +38,56 @@ run_ab() {
   cat $out/ab.log
 }
 
+# variant 77 (320 x 256 balanced c_fc tile): kernel tests, kernel A/B against v75, in-model A/B
+run_t320() {
+  out=gpurun_out/r06_t320
+  mkdir -p $out
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread \
+    -k "77 or race" > $out/kernels.log 2>&1 || { echo "kernel tests failed"; tail -30 $out/kernels.log; exit 1; }
+  tail -2 $out/kernels.log
+  timeout -k 10 300 python -u tools/gemm_ab.py "12800,3072,768,1;12800,2304,768,0" "13475,13477,3475,3477,98,13472" 5 20 \
+    > $out/gemm_ab.log 2>&1 || { echo "gemm_ab failed"; tail -10 $out/gemm_ab.log; exit 1; }
+  cat $out/gemm_ab.log
+  timeout -k 10 900 bash tools/ab_envs.sh "--steps 20 --warmup 5" 3 - "--tuning fc_balanced_variant=77" > $out/ab.log 2>&1 \
+    || { echo "A/B failed"; tail -20 $out/ab.log; exit 1; }
+  cat $out/ab.log
+}
+
+# The GEMM k-loop split into phases: the stamped shipped kernel (gemm_probe
+# p32, hook policy P32Stamp) on the c_fc shape as shipped (balanced grid, map 34) and on the QKV
+# shape, the ablations, then per-role PMC passes of the default bench (LDS / VMEM issue, TA, TCP).
+run_phases() {
+  R=$GRAFT_REPO_ROOT
+  out=$R/gpurun_out/r06_phases
+  mkdir -p $out
+  P=$R/tools/probes/gemm_probe
+  { echo "== c_fc 12800x3072x768 gelu xcd34 balanced"; timeout -k 10 120 $P p32 12800 3072 768 1 34 1 && \
+    echo "== QKV 12800x2304x768 store xcd0"; timeout -k 10 120 $P p32 12800 2304 768 0 0 0; } > $out/stamps.txt 2>&1 \
+    || { echo "probe failed"; tail -20 $out/stamps.txt; exit 1; }
+  cat $out/stamps.txt
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 60 rocprofv3 -L > $out/counters.txt 2>&1 || echo "counter list failed"
+  grep -oE "(TA_[A-Z_]+|TCP_PENDING[A-Z_]*|SQ_INST_CYCLES_VMEM|SQ_WAIT_INST_LDS|SQ_INSTS_LDS)" $out/counters.txt | sort -u | head -40 || true
+  B="python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --profile-iters 1"
+  i=0
+  for set in "SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" \
+             "TA_BUSY_avr TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum GRBM_GUI_ACTIVE" \
+             "TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum" \
+             "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY"; do
+    i=$((i+1))
+    timeout -s KILL 150 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $out/pmc$i -o run -- $B > $out/pmc$i.log 2>&1 \
+      || { rc=$?; echo "pass $i ($set) failed rc=$rc"; tail -3 $out/pmc$i.log; [ $rc -ge 124 ] && exit 1; }
+  done
+  echo phases-done
+}
+
 recipe=${1:-}
 shift || true
 case "$recipe" in
   check) run_check "$@" ;;
   tests) run_tests "$@" ;;
   ab) run_ab "$@" ;;
+  t320) run_t320 "$@" ;;
+  phases) run_phases "$@" ;;
   *) echo "recipes: check | tests <expr> [files] | ab '<bench args>' R arm..."; exit 2 ;;
 esac
