@@ -273,6 +273,11 @@ struct clipvit_handle {
     // copies). tuning w_blocked. B/32 bs 256: 87.2-87.4k -> 88.0-88.6k img/s against 0 (QKV 0.578 ->
     // 0.565, c_proj 0.627 -> 0.610 ms per forward; same box, profiles/r05/b32_final_wblk_ab.txt)
     int w_blk = 2;
+    // the LayerNorm output h (QKV's and c_fc's A operand) in the 16-row blocked layout on the
+    // 24-bit-residual forward: the LN kernels write it through an LDS transpose, and the QKV / c_fc
+    // staging fetches 1 KB runs (128-B L2 requests) instead of 64-B row pieces (tuning h_blocked)
+    bool h_blk = false;
+    bool use_hblk() const { return h_blk && use_x24() && !lnfold; }
     // test hook (tuning trace_gemm=1): every role GEMM launch of gemm() / gemm8() appends
     // {role, tile variant, M, flags} here (clipvit_gemm_log), so a test can assert which kernel
     // path a configuration reaches. Off in the product path.
@@ -446,7 +451,7 @@ struct Fold {
 
 static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const void* W,
                 const float* bias, void* C, int M, int N, int K, int ldc, int role, const Fold& fo = Fold(),
-                Lane* lane = nullptr, const void* Wb = nullptr) {
+                Lane* lane = nullptr, const void* Wb = nullptr, bool ablk = false) {
     GemmArgs a{};
     a.A = A; a.W = W; a.bias = bias; a.C = C;
     a.M = M; a.N = N; a.K = K; a.ldc = ldc;
@@ -460,7 +465,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     auto blk_ok = [](int v) { return v >= 8; };
     const bool ublk = h->u_blk && (!h->var_forced || (blk_ok(h->var[R_FC]) && blk_ok(h->var[R_PROJ])));
     a.blk_c = ublk && role == R_FC;
-    a.blk_a = ublk && role == R_PROJ;
+    a.blk_a = (ublk && role == R_PROJ) || ablk;  // ablk: A = h in the blocked layout (use_hblk)
     int variant = h->var[role];
     auto launch = [&](const GemmArgs& g, int v) {
         const int rc = launch_gemm(s, h->dt, epi, g, v);
@@ -897,8 +902,9 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     const LayerW& l0 = h->layers[0];
     // X24: the residual stream in 24-bit planes (w->x then only holds the patch GEMM's rows)
     void* X24 = h->use_x24() ? w->x16 : nullptr;
+    const bool hb = h->use_hblk();
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
-                    B, N, D, X24, X24 != nullptr);
+                    B, N, D, X24, X24 != nullptr, hb);
     if (prof) prof->mark(s, F_EMBED);
     // 16-bit residual branch outputs (resid16) reuse the qkv buffer: qkv is dead once attention
     // has read it. y = out_proj's branch, y2 = c_proj's. With deferred adds (defer_x), the add
@@ -910,7 +916,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
         const bool last = i + 1 == nl;
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b)))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b, hb)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
@@ -924,7 +930,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         if (h->resid16) {
             if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT, Fold(), w, ly.wout_b))) return rc;
             if (prof) prof->mark(s, F_OUT);
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D, X24, X24 != nullptr);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D, X24, X24 != nullptr, hb);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, ly.ln2g, ly.ln2b, M, D);
         } else {
             if ((rc = gemm(s, h, EPI_RESID, w->h, ly.wout, ly.bout, w->x, M, D, D, D, R_OUT))) return rc;
@@ -932,7 +938,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
         }
         if (prof) prof->mark(s, F_LN);
-        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b)))
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b, hb)))
             return rc;
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
@@ -941,7 +947,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                 return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr, hb);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -1172,6 +1178,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "trace_gemm") ok = flag(h->trace);
+    else if (k == "h_blocked") ok = flag(h->h_blk);
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
@@ -1232,14 +1239,14 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace, h_blk;
         int w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1255,7 +1262,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1641,9 +1648,23 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     void* Wp = nullptr;
     HIPCHK(hipMallocAsync(&Wp, (size_t)N * K * 2, s));
     launch_pack_weight(s, dtype, (const float*)W_dev, Wp, N, K, K);
-    const bool wblk = variant >= 10000;  // + 10000: W in the blocked layout (GemmArgs.blk_w)
+    // + 10000: W in the blocked layout (GemmArgs.blk_w); + 20000: A too (GemmArgs.blk_a, a
+    // blocked copy of A_dev with the rows padded to 16); + 30000: both
+    const bool wblk = (variant / 10000) & 1, ablk = ((variant / 10000) >> 1) & 1;
     variant %= 10000;
     if (wblk && N % 16) FAIL(CLIPVIT_E_INVALID, "blocked W needs N % 16 == 0");
+    void* Ab = nullptr;
+    if (ablk) {
+        const int mp = (M + 15) / 16 * 16;
+        HIPCHK(hipMallocAsync(&Ab, (size_t)mp * K * 2, s));
+        HIPCHK(hipMemsetAsync(Ab, 0, (size_t)mp * K * 2, s));
+        void* Ap = nullptr;  // A with zero padding rows, then relaid out
+        HIPCHK(hipMallocAsync(&Ap, (size_t)mp * K * 2, s));
+        HIPCHK(hipMemsetAsync(Ap, 0, (size_t)mp * K * 2, s));
+        HIPCHK(hipMemcpyAsync(Ap, A_dev, (size_t)M * K * 2, hipMemcpyDeviceToDevice, s));
+        launch_blk16_relayout(s, Ap, Ab, mp, K);
+        HIPCHK(hipFreeAsync(Ap, s));
+    }
     if (wblk) {  // relayout in place through a copy
         void* Wr = nullptr;
         HIPCHK(hipMallocAsync(&Wr, (size_t)N * K * 2, s));
@@ -1652,10 +1673,11 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         HIPCHK(hipFreeAsync(Wr, s));
     }
     GemmArgs a{};
-    a.A = A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
+    a.A = ablk ? Ab : A_dev; a.W = Wp; a.bias = bias_dev; a.C = C_dev;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.ncu = current_ncu();
     a.blk_w = wblk;
+    a.blk_a = ablk;
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
@@ -1671,6 +1693,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         if (epi >= 10) epi -= 10;
         if (epi == 2) {
             hipFreeAsync(Wp, s);
+            if (Ab) hipFreeAsync(Ab, s);
             FAIL(CLIPVIT_E_INVALID, "variant has no residual epilogue");
         }
         void* C16 = nullptr;
@@ -1684,6 +1707,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
         rc = launch_gemm(s, dtype, e, a, variant);
     }
     HIPCHK(hipFreeAsync(Wp, s));
+    if (Ab) HIPCHK(hipFreeAsync(Ab, s));
     if (rc) FAIL(CLIPVIT_E_INVALID, "unsupported gemm shape/variant");
     HIPCHK(hipGetLastError());
     return 0;
@@ -1761,9 +1785,13 @@ int clipvit_gemm_bench(int dtype, int M, int N, int K, int epi, int variant, int
     a.A = A; a.W = W; a.bias = bias; a.C = Cb;
     a.M = M; a.N = N; a.K = K; a.ldc = N;
     a.patch_g2 = 49; a.patch_ntok = 50;
-    a.blk_w = variant >= 10000;  // (random operands: the layout only changes the access pattern)
+    // + 10000: blocked W, + 20000: blocked A, + 30000: both (random operands: the layout only
+    // changes the access pattern)
+    a.blk_w = (variant / 10000) & 1;
+    a.blk_a = ((variant / 10000) >> 1) & 1;
     variant %= 10000;
     if (a.blk_w && N % 16) FAIL(CLIPVIT_E_INVALID, "blocked W needs N % 16 == 0");
+    if (a.blk_a && M % 16) FAIL(CLIPVIT_E_INVALID, "blocked A needs M % 16 == 0");
     a.xcd_n = variant / 100;
     variant %= 100;
     a.ncu = current_ncu();

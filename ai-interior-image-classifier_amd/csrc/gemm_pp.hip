@@ -300,11 +300,18 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
     const int grid = ntiles < ncu ? ntiles : ncu;
-    if (a.blk_a) {  // blocked A (u): c_proj on the persistent tile (tuning / large-M shapes)
-        if (epi != EPI_STORE) return -1;
-        if (a.blk_w) gemm_ppp_kernel<T, EPI_STORE, NT, true, true><<<grid, 512, 0, s>>>(a, ntiles);
-        else gemm_ppp_kernel<T, EPI_STORE, NT, true><<<grid, 512, 0, s>>>(a, ntiles);
-        return 0;
+    if (a.blk_a) {  // blocked A: c_proj's u, or h in the 16-row blocked layout (QKV / c_fc)
+        if (epi == EPI_STORE) {
+            if (a.blk_w) gemm_ppp_kernel<T, EPI_STORE, NT, true, true><<<grid, 512, 0, s>>>(a, ntiles);
+            else gemm_ppp_kernel<T, EPI_STORE, NT, true><<<grid, 512, 0, s>>>(a, ntiles);
+            return 0;
+        }
+        if (epi == EPI_GELU) {
+            if (a.blk_w) gemm_ppp_kernel<T, EPI_GELU, NT, true, true><<<grid, 512, 0, s>>>(a, ntiles);
+            else gemm_ppp_kernel<T, EPI_GELU, NT, true><<<grid, 512, 0, s>>>(a, ntiles);
+            return 0;
+        }
+        return -1;
     }
     if (a.blk_w) {  // blocked W
         if (epi == EPI_STORE) { gemm_ppp_kernel<T, EPI_STORE, NT, false, true><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
@@ -324,8 +331,9 @@ static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a, bool balanced
     const int ntiles = ((a.M + BM - 1) / BM) * (a.N / 256);
     const int per = (ntiles + ncu - 1) / ncu;
     const int grid = balanced ? (ntiles + per - 1) / per : ntiles < ncu ? ntiles : ncu;
-    if (a.blk_a) {  // blocked A (u): c_proj
+    if (a.blk_a) {  // blocked A: c_proj's u, or h in the 16-row blocked layout (QKV / c_fc)
         if (epi == EPI_STORE) { gemm_p32_kernel<T, EPI_STORE, true, BLKW, NT, BM><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+        if (epi == EPI_GELU) { gemm_p32_kernel<T, EPI_GELU, true, BLKW, NT, BM><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
         return -1;
     }
     if (epi == EPI_STORE) { gemm_p32_kernel<T, EPI_STORE, false, BLKW, NT, BM><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
@@ -344,7 +352,6 @@ static int launch_p32(hipStream_t s, int epi, const GemmArgs& a, bool nt, bool b
 // bytes on the busiest CU)
 template <typename T>
 static int launch_p32_320(hipStream_t s, int epi, const GemmArgs& a) {
-    if (a.blk_a) return -1;  // the 16-row blocked A of c_proj: 256-row tiles only
     return a.blk_w ? launch_p32_t<T, true, false, 320>(s, epi, a, true) : launch_p32_t<T, false, false, 320>(s, epi, a, true);
 }
 

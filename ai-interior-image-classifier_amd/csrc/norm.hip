@@ -130,6 +130,26 @@ __device__ __forceinline__ float4 unpack4_f16(uint2 w) {
 
 // 24-bit residual rows (X24): x24_load / x24_store, common.h.
 
+// 16-bit LayerNorm output h in the 16-row blocked layout (blk16_off), the A operand form whose
+// 32-deep k-step of a 16-row block is one contiguous 1 KB run (128-B L2 requests for the
+// QKV / c_fc staging instead of 64-B row pieces). Direct form (embed_ln: once per forward): the
+// lane's 4 columns are 8 B at blk16_off.
+template <typename T, int V>
+__device__ __forceinline__ void store_row16_blk(u16* h, int row, const float4 (&v)[V], int lane) {
+    constexpr int D = 256 * V;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        *(uint2*)((unsigned char*)h + blk16_off(row, c, D)) = make_uint2(pack2<T>(v[i].x, v[i].y), pack2<T>(v[i].z, v[i].w));
+    }
+}
+// LDS image of one 16-row group in the blocked order, with the row slot of (block b, chunk c)
+// XOR-ed by c | (b & 1) << 3: a wave's writes of one row then spread over 32 banks (2-way) instead
+// of 4, and a quarter-wave's 16-B reads of one chunk (16 row slots) stay conflict-free.
+__device__ __forceinline__ int hblk_lds_off(int b, int c, int m) {
+    return (b << 11) + (c << 8) + ((m ^ (c | ((b & 1) << 3))) << 4);
+}
+
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
 // E8M0 scale (rule: common.h mx_exp).
@@ -154,7 +174,7 @@ __device__ __forceinline__ void store_row_q8(unsigned char* q, unsigned char* sq
 // (Q8: h as MX-fp8 q [rows][D] + scales sq [rows][D/32])
 // X16 (MX-fp8 forward, fp16 residual stream): x holds the patch GEMM's fp32 rows (read only) and
 // the residual goes to x16 as fp16.
-template <typename T, int V, bool Q8 = false, bool X16 = false, bool X24 = false>
+template <typename T, int V, bool Q8 = false, bool X16 = false, bool X24 = false, bool BLKH = false>
 __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, void* __restrict__ h,
                                                        unsigned char* __restrict__ sq,
                                                        const float* __restrict__ cls,
@@ -192,6 +212,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
     }
     ln_row<V>(v, g1, b1, lane, (float)D);
     if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v, lane);
+    else if constexpr (BLKH) store_row16_blk<T, V>((u16*)h, row, v, lane);
     else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
@@ -308,18 +329,22 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // Q8: h is the MX-fp8 A operand of the next GEMM (q [rows][D] + E8M0 scales sq [rows][D/32]).
 // X16: x is the fp16 residual stream (u16 storage) instead of fp32; the sum and the LayerNorm are
 // fp32, the stored x is its fp16 rounding.
+// BLKH: h in the 16-row blocked layout; RPW = 4, so a workgroup owns one 16-row group: its rows'
+// outputs go to LDS in the blocked order and leave as one contiguous run (32 D bytes). Rows past
+// `rows` in the last group (padding rows of the buffer) carry the last row's values.
 template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false,
-          bool X24 = false>
+          bool X24 = false, bool BLKH = false>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ xv, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
                                                             const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
+    static_assert(!BLKH || (RPW == 4 && !Q8), "blocked h: 16 rows per workgroup, 16-bit output");
     // RPW rows per wave, every row's loads issued before any row's arithmetic (more bytes in
     // flight per wave; rows / RPW waves fit one residency round of the CUs at bs 256)
     const int lane = threadIdx.x & 63;
     const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-    if (row0 >= rows) return;
+    if (!BLKH && row0 >= rows) return;  // (BLKH: every wave reaches the barrier below)
     constexpr int D = 256 * V;
     float* const x = (float*)xv;
     u16* const x16 = (u16*)xv;
@@ -340,10 +365,13 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
             if constexpr (TWO) w2[r][i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
         }
     }
+    constexpr int HLDS = BLKH ? 32 * D : 16;
+    __shared__ __attribute__((aligned(16))) unsigned char hs[HLDS];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-        const int row = row0 + r;
-        if (row >= rows) break;
+        const int row = BLKH ? min(row0 + r, rows - 1) : row0 + r;
+        if (!BLKH && row >= rows) break;
+        const bool own = row0 + r < rows;  // (BLKH: a padding row stores no x)
         float* xr = x + (size_t)row * D;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -358,14 +386,30 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
                 v[r][i].z += T::to_f32((u16)(w2[r][i].y & 0xffff));
                 v[r][i].w += T::to_f32((u16)(w2[r][i].y >> 16));
             }
-            if constexpr (STORE_X && X24)
-                x24_store((unsigned char*)xv, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4, v[r][i]);
-            else if constexpr (STORE_X && !X16) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
+            if constexpr (STORE_X && X24) {
+                if (own) x24_store((unsigned char*)xv, (size_t)rows * D * 2, (size_t)row * D + (lane + 64 * i) * 4, v[r][i]);
+            } else if constexpr (STORE_X && !X16) {
+                if (own) *(float4*)(xr + (lane + 64 * i) * 4) = v[r][i];
+            }
         }
         if constexpr (STORE_X && X16) store_x16<V>(x16 + (size_t)row * D, v[r], lane);
         ln_row<V>(v[r], gm, bt, lane, (float)D);
         if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v[r], lane);
-        else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
+        else if constexpr (BLKH) {
+            const int m = (threadIdx.x >> 6) * RPW + r;  // row slot inside the 16-row group
+#pragma unroll
+            for (int i = 0; i < V; ++i) {
+                const int c = (lane + 64 * i) * 4;
+                const int off = hblk_lds_off(c >> 6, (c & 63) >> 3, m) + ((c & 7) << 1);
+                *(uint2*)(hs + off) = make_uint2(pack2<T>(v[r][i].x, v[r][i].y), pack2<T>(v[r][i].z, v[r][i].w));
+            }
+        } else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
+    }
+    if constexpr (BLKH) {  // the group's 32 D bytes, contiguous in the blocked layout
+        __syncthreads();
+        unsigned char* dst = (unsigned char*)h + (size_t)blockIdx.x * 32 * D;
+        for (int o = threadIdx.x * 16; o < 32 * D; o += 256 * 16)
+            *(uint4*)(dst + o) = *(const uint4*)(hs + hblk_lds_off(o >> 11, (o >> 8) & 7, (o >> 4) & 15));
     }
 }
 
@@ -447,10 +491,15 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D, void* x16, bool x24) {
+                     const float* b1, int B, int N, int D, void* x16, bool x24, bool hblk) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
     u16* xo = (u16*)x16;
+    if (x24 && hblk) {
+        if (dtype == 2) DISPATCH_V(D, embed_ln_kernel<F16, V, false, false, true, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        else DISPATCH_V(D, embed_ln_kernel<BF16, V, false, false, true, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
+        return;
+    }
     if (x24) {
         if (dtype == 2) DISPATCH_V(D, embed_ln_kernel<F16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
         else DISPATCH_V(D, embed_ln_kernel<BF16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
@@ -516,9 +565,15 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
     }
 }
 
-template <typename T, int V, bool X16, bool X24 = false>
+template <typename T, int V, bool X16, bool X24 = false, bool BLKH = false>
 static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
+    if constexpr (BLKH) {  // one workgroup per 16-row group (4 waves x 4 rows)
+        dim3 grid((rows + 15) / 16), block(256);
+        if (y2) add_layernorm_kernel<T, V, true, true, 4, false, X16, X24, true><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 4, false, X16, X24, true><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+        return;
+    }
     dim3 grid((rows + 3) / 4), block(256);
     if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
     else add_layernorm_kernel<T, V, false, false, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
@@ -564,8 +619,14 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
 }
 
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
-                                   void* h, const float* g, const float* b, int rows, int D, void* x16, bool x24) {
+                                   void* h, const float* g, const float* b, int rows, int D, void* x16, bool x24,
+                                   bool hblk) {
     const u16 *yy = (const u16*)y, *yy2 = (const u16*)y2;
+    if (x24 && hblk) {
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        return;
+    }
     if (x24) {
         if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))

@@ -245,7 +245,8 @@ int clipvit_resample_plan(int in_size, int out_size, int* ksize, int* bounds, in
  * products without bias; K % (64 S) == 0 — the class-token tail's GEMMs). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
  * N % 256 for variant 3). variant % 100 selects the tile kernel (0 auto; the table in
  * csrc/gemm.hip pick/launch_gemm); variant / 100 the block->XCD mapping
- * (0/1 = 1-D bijective remap, 2 = 4x2 (M-band, N-half) partition; pipelined variants only).
+ * (0/1 = 1-D bijective remap, 2 = 4x2 (M-band, N-half) partition; pipelined variants only);
+ * + 10000 = W in the 16-row blocked layout, + 20000 = A blocked, + 30000 = both.
  * The same encoding applies to clipvit_gemm_bench. */
 int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_dev,
                       const float* bias_dev, float* C_dev, int M, int N, int K, int epi,

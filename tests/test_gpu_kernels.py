@@ -284,3 +284,23 @@ def test_residual_x24_round_trip(gpu):
     nz = x != 0
     rel = ((back - x).abs()[nz] / x.abs()[nz]).max().item()
     assert rel <= 2.0 ** -16, rel
+
+
+@pytest.mark.parametrize("variant", [8, 22, 62, 72, 75, 77, 80, 81, 82, 98, 298, 3475, 3477])
+@pytest.mark.parametrize("M,N,K", [(1000, 2304, 768), (12800, 3072, 768)])
+def test_blocked_a_is_bit_identical(gpu, variant, M, N, K):
+    """A (the LayerNorm output h that QKV / c_fc read) in the 16-row blocked layout (+ 20000; with
+    the blocked weight copy + 30000) moves bytes only: every tile stages the same k-slices into
+    the same LDS image, so the 16-bit STORE / QuickGELU outputs equal the row-major run's bit for
+    bit, ragged M included."""
+    if N % (256 if variant % 100 in N256 else 128):
+        pytest.skip("tile does not divide N")
+    g = torch.Generator(device=gpu).manual_seed(M + K + 7)
+    A = torch.randn(M, K, device=gpu, generator=g).to(torch.float16)
+    W = torch.randn(N, K, device=gpu, generator=g) * 0.05
+    bias = torch.randn(N, device=gpu, generator=g)
+    for epi in (10, 11):
+        ref = E.gemm_test(A, W, bias, epi=epi, variant=variant)
+        for v in (20000 + variant, 30000 + variant):
+            C = E.gemm_test(A, W, bias, epi=epi, variant=v)
+            assert torch.equal(C, ref), (v, epi, (C - ref).abs().max().item())

@@ -81,6 +81,25 @@ run_phases() {
   echo phases-done
 }
 
+# blocked A (h in the 16-row blocked layout): kernel bit-identity, then kernel A/B on the B/32
+# c_fc (v75) and QKV (v98) shapes, row-major A against blocked A (both with blocked W)
+run_ablk() {
+  out=gpurun_out/r06_ablk
+  mkdir -p $out
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread \
+    -k "blocked_a" > $out/kernels.log 2>&1 || { echo "kernel tests failed"; tail -30 $out/kernels.log; exit 1; }
+  tail -2 $out/kernels.log
+  timeout -k 10 400 python -u tools/gemm_ab.py "12800,3072,768,1;12800,2304,768,0;6400,3072,768,1" "13475,33475,10298,30298,13462,33462" 7 20 \
+    > $out/gemm_ab.log 2>&1 || { echo "gemm_ab failed"; tail -10 $out/gemm_ab.log; exit 1; }
+  cat $out/gemm_ab.log
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread \
+    -k "blocked_h" > $out/parity.log 2>&1 || { echo "parity tests failed"; tail -30 $out/parity.log; exit 1; }
+  tail -2 $out/parity.log
+  timeout -k 10 900 bash tools/ab_envs.sh "--steps 20 --warmup 5" 3 - "--tuning h_blocked=1" > $out/ab.log 2>&1 \
+    || { echo "A/B failed"; tail -20 $out/ab.log; exit 1; }
+  cat $out/ab.log
+}
+
 recipe=${1:-}
 shift || true
 case "$recipe" in
@@ -89,5 +108,6 @@ case "$recipe" in
   ab) run_ab "$@" ;;
   t320) run_t320 "$@" ;;
   phases) run_phases "$@" ;;
+  ablk) run_ablk "$@" ;;
   *) echo "recipes: check | tests <expr> [files] | ab '<bench args>' R arm..."; exit 2 ;;
 esac
