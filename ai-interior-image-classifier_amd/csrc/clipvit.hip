@@ -273,11 +273,15 @@ struct clipvit_handle {
     // copies). tuning w_blocked. B/32 bs 256: 87.2-87.4k -> 88.0-88.6k img/s against 0 (QKV 0.578 ->
     // 0.565, c_proj 0.627 -> 0.610 ms per forward; same box, profiles/r05/b32_final_wblk_ab.txt)
     int w_blk = 2;
-    // the LayerNorm output h (QKV's and c_fc's A operand) in the 16-row blocked layout on the
-    // 24-bit-residual forward: the LN kernels write it through an LDS transpose, and the QKV / c_fc
-    // staging fetches 1 KB runs (128-B L2 requests) instead of 64-B row pieces (tuning h_blocked)
-    bool h_blk = false;
-    bool use_hblk() const { return h_blk && use_x24() && !lnfold; }
+    // ln_2's output h (c_fc's A operand) in the 16-row blocked layout on the 24-bit-residual
+    // forward, so the c_fc staging fetches 1 KB runs (128-B L2 requests) instead of 64-B row
+    // pieces (tuning h_blocked: 2 = through an LDS transpose in the LN kernel, the default; 1 = the
+    // LN kernel's lanes store 8 B each at blk16_off; 0 = row-major). Same box, 3 alternations:
+    // B/32 bs 256 83.45-83.49k -> 83.76-84.14k img/s with 2 (c_fc 0.81 -> 0.784 ms per forward,
+    // LayerNorm +0.018), 83.08-83.48k with 1 (profiles/r06/hblk_inmodel_ab.txt). QKV's h stays
+    // row-major: its 240x256 tile measured the same either way (profiles/r06/hblk_v1_inmodel_ab.txt)
+    int h_blk = 2;
+    int use_hblk() const { return use_x24() && !lnfold ? h_blk : 0; }
     // test hook (tuning trace_gemm=1): every role GEMM launch of gemm() / gemm8() appends
     // {role, tile variant, M, flags} here (clipvit_gemm_log), so a test can assert which kernel
     // path a configuration reaches. Off in the product path.
@@ -902,9 +906,9 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     const LayerW& l0 = h->layers[0];
     // X24: the residual stream in 24-bit planes (w->x then only holds the patch GEMM's rows)
     void* X24 = h->use_x24() ? w->x16 : nullptr;
-    const bool hb = h->use_hblk();
+    const int hb = h->use_hblk();
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
-                    B, N, D, X24, X24 != nullptr, hb);
+                    B, N, D, X24, X24 != nullptr);
     if (prof) prof->mark(s, F_EMBED);
     // 16-bit residual branch outputs (resid16) reuse the qkv buffer: qkv is dead once attention
     // has read it. y = out_proj's branch, y2 = c_proj's. With deferred adds (defer_x), the add
@@ -916,7 +920,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
         const bool last = i + 1 == nl;
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b, hb)))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
@@ -938,7 +942,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             launch_layernorm(s, h->dt, w->x, w->h, ly.ln2g, ly.ln2b, M, D);
         }
         if (prof) prof->mark(s, F_LN);
-        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b, hb)))
+        if ((rc = gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b, hb != 0)))
             return rc;
         if (prof) prof->mark(s, F_FC);
         if (h->resid16 && !last) {
@@ -947,7 +951,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                 return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr, hb);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -1178,7 +1182,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "trace_gemm") ok = flag(h->trace);
-    else if (k == "h_blocked") ok = flag(h->h_blk);
+    else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 2;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
@@ -1239,8 +1243,8 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace, h_blk;
-        int w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
+        int h_blk, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };

@@ -366,10 +366,11 @@ void launch_splitk_resid_ln(hipStream_t s, int dtype, float* x, const float* P, 
 void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const float* bias, void* u, int rows,
                         int n);
 // x24 = true: x16 is instead the 24-bit residual stream of the 16-bit forward (norm.hip x24_load);
-// hblk = true (with x24): h in the 16-row blocked layout (blk16_off), rows padded to 16
+// hblk (with x24): h in the 16-row blocked layout (blk16_off), rows padded to 16; 1 = direct
+// stores, 2 = through an LDS transpose (norm.hip add_layernorm_kernel HBLK)
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
                                    void* h, const float* g, const float* b, int rows, int D, void* x16 = nullptr,
-                                   bool x24 = false, bool hblk = false);
+                                   bool x24 = false, int hblk = 0);
 void launch_x24_roundtrip(hipStream_t s, const float* x, void* planes, float* back, size_t n);
 void launch_gather_cls(hipStream_t s, const float* x, const void* h, float* xc, void* hc, int B, int N, int D,
                        const void* x16 = nullptr, bool x24 = false);
@@ -404,8 +405,7 @@ void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int 
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D, void* x16 = nullptr, bool x24 = false,
-                     bool hblk = false);
+                     const float* b1, int B, int N, int D, void* x16 = nullptr, bool x24 = false);
 void launch_layernorm(hipStream_t s, int dtype, const float* x, void* h, const float* g,
                       const float* b, int rows, int D);
 void launch_pack_weight(hipStream_t s, int dtype, const float* src, void* dst, int N, int K,

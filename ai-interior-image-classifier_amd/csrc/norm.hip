@@ -131,9 +131,8 @@ __device__ __forceinline__ float4 unpack4_f16(uint2 w) {
 // 24-bit residual rows (X24): x24_load / x24_store, common.h.
 
 // 16-bit LayerNorm output h in the 16-row blocked layout (blk16_off), the A operand form whose
-// 32-deep k-step of a 16-row block is one contiguous 1 KB run (128-B L2 requests for the
-// QKV / c_fc staging instead of 64-B row pieces). Direct form (embed_ln: once per forward): the
-// lane's 4 columns are 8 B at blk16_off.
+// 32-deep k-step of a 16-row block is one contiguous 1 KB run (128-B L2 requests for the c_fc
+// staging instead of 64-B row pieces). Direct form: the lane's 4 columns are 8 B at blk16_off.
 template <typename T, int V>
 __device__ __forceinline__ void store_row16_blk(u16* h, int row, const float4 (&v)[V], int lane) {
     constexpr int D = 256 * V;
@@ -174,7 +173,7 @@ __device__ __forceinline__ void store_row_q8(unsigned char* q, unsigned char* sq
 // (Q8: h as MX-fp8 q [rows][D] + scales sq [rows][D/32])
 // X16 (MX-fp8 forward, fp16 residual stream): x holds the patch GEMM's fp32 rows (read only) and
 // the residual goes to x16 as fp16.
-template <typename T, int V, bool Q8 = false, bool X16 = false, bool X24 = false, bool BLKH = false>
+template <typename T, int V, bool Q8 = false, bool X16 = false, bool X24 = false>
 __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, void* __restrict__ h,
                                                        unsigned char* __restrict__ sq,
                                                        const float* __restrict__ cls,
@@ -212,7 +211,6 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
     }
     ln_row<V>(v, g1, b1, lane, (float)D);
     if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v, lane);
-    else if constexpr (BLKH) store_row16_blk<T, V>((u16*)h, row, v, lane);
     else store_row16<T, V>((u16*)h + (size_t)row * D, v, lane);
 }
 
@@ -329,17 +327,21 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // Q8: h is the MX-fp8 A operand of the next GEMM (q [rows][D] + E8M0 scales sq [rows][D/32]).
 // X16: x is the fp16 residual stream (u16 storage) instead of fp32; the sum and the LayerNorm are
 // fp32, the stored x is its fp16 rounding.
-// BLKH: h in the 16-row blocked layout; RPW = 4, so a workgroup owns one 16-row group: its rows'
-// outputs go to LDS in the blocked order and leave as one contiguous run (32 D bytes). Rows past
-// `rows` in the last group (padding rows of the buffer) carry the last row's values.
+// HBLK: h in the 16-row blocked layout (blk16_off). 1: every lane stores its 8 B at blk16_off
+// (a wave-instruction writes 32 scattered 16-B chunks). 2: RPW = 4, so a workgroup owns one 16-row
+// group: its rows' outputs go to LDS in the blocked order and leave as one contiguous run (32 D
+// bytes); rows past `rows` in the last group (padding rows of the buffer) carry the last row's
+// values.
 template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false,
-          bool X24 = false, bool BLKH = false>
+          bool X24 = false, int HBLK = 0>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ xv, const u16* __restrict__ y,
                                                             const u16* __restrict__ y2,
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
                                                             const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
+    constexpr bool BLKH = HBLK == 2;
     static_assert(!BLKH || (RPW == 4 && !Q8), "blocked h: 16 rows per workgroup, 16-bit output");
+    static_assert(HBLK != 1 || !Q8, "blocked h: 16-bit output");
     // RPW rows per wave, every row's loads issued before any row's arithmetic (more bytes in
     // flight per wave; rows / RPW waves fit one residency round of the CUs at bs 256)
     const int lane = threadIdx.x & 63;
@@ -403,6 +405,8 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
                 const int off = hblk_lds_off(c >> 6, (c & 63) >> 3, m) + ((c & 7) << 1);
                 *(uint2*)(hs + off) = make_uint2(pack2<T>(v[r][i].x, v[r][i].y), pack2<T>(v[r][i].z, v[r][i].w));
             }
+        } else if constexpr (HBLK == 1) {
+            store_row16_blk<T, V>((u16*)h, row, v[r], lane);
         } else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
     }
     if constexpr (BLKH) {  // the group's 32 D bytes, contiguous in the blocked layout
@@ -491,15 +495,10 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,
-                     const float* b1, int B, int N, int D, void* x16, bool x24, bool hblk) {
+                     const float* b1, int B, int N, int D, void* x16, bool x24) {
     const int rows = B * N;
     dim3 grid((rows + 3) / 4), block(256);
     u16* xo = (u16*)x16;
-    if (x24 && hblk) {
-        if (dtype == 2) DISPATCH_V(D, embed_ln_kernel<F16, V, false, false, true, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
-        else DISPATCH_V(D, embed_ln_kernel<BF16, V, false, false, true, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
-        return;
-    }
     if (x24) {
         if (dtype == 2) DISPATCH_V(D, embed_ln_kernel<F16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
         else DISPATCH_V(D, embed_ln_kernel<BF16, V, false, false, true><<<grid, block, 0, s>>>(x, h, nullptr, cls, pos, g_pre, b_pre, g1, b1, rows, N, xo))
@@ -565,18 +564,18 @@ void launch_add_layernorm(hipStream_t s, int dtype, float* x, const void* y, voi
     }
 }
 
-template <typename T, int V, bool X16, bool X24 = false, bool BLKH = false>
+template <typename T, int V, bool X16, bool X24 = false, int HBLK = 0>
 static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2, u16* h, const float* g,
                             const float* b, int rows) {
-    if constexpr (BLKH) {  // one workgroup per 16-row group (4 waves x 4 rows)
+    if constexpr (HBLK == 2) {  // one workgroup per 16-row group (4 waves x 4 rows)
         dim3 grid((rows + 15) / 16), block(256);
-        if (y2) add_layernorm_kernel<T, V, true, true, 4, false, X16, X24, true><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
-        else add_layernorm_kernel<T, V, false, false, 4, false, X16, X24, true><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
-        return;
+        if (y2) add_layernorm_kernel<T, V, true, true, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+    } else {
+        dim3 grid((rows + 3) / 4), block(256);
+        if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16, X24, HBLK><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 1, false, X16, X24, HBLK><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
     }
-    dim3 grid((rows + 3) / 4), block(256);
-    if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
-    else add_layernorm_kernel<T, V, false, false, 1, false, X16, X24><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
 }
 
 // MX-fp8 forms (bf16 branch outputs): y2 given -> x = (x + y) + y2 stored; y2 null -> x + y not
@@ -620,11 +619,16 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
 
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
                                    void* h, const float* g, const float* b, int rows, int D, void* x16, bool x24,
-                                   bool hblk) {
+                                   int hblk) {
     const u16 *yy = (const u16*)y, *yy2 = (const u16*)y2;
-    if (x24 && hblk) {
-        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
-        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, true>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+    if (x24 && hblk == 1) {
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 1>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 1>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        return;
+    }
+    if (x24 && hblk == 2) {
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         return;
     }
     if (x24) {
