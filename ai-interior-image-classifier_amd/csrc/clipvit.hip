@@ -159,7 +159,7 @@ struct clipvit_handle {
     int var[5] = {98, 82, 22, 82, 22};
     bool var_forced = false;  // tuning gemm_variants given: no shape-based override
     // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
-    // tile; 0 = the 2-phase tiles (80 / 8). Default: the persistent ping-pong tile with the
+    // tile; 0 = the 2-phase 256x256 tile (8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
     // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
     // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
@@ -498,7 +498,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // bit-identical to one launch. Measured (c_fc 12800 x 3072 x 768): 81.6 us in one launch
     // (128x128) or 77.6 (256x256, 3 rounds) -> 54.3 + 15.9 = 70.2 us.
     // the main launch's tile width: every pipelined variant a round split can use is 256 wide
-    // (8 / 80: 256x256, 98: 240x256)
+    // (8 / 62 / 72 / 74: 256x256, 98: 240x256)
     const int bn = 256;
     // (the ping-pong main tiles, split_main >= 60, have the 16-bit STORE / GELU epilogues only:
     // the LayerNorm-fold epilogues take the single-launch path below)
@@ -546,7 +546,7 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
     // c_fc 7.79 -> 7.52 ms, B/16 1.59 -> 1.52 ms per lane-forward against the LDS-staged v80)
     if (!h->var_forced && role != R_PATCH &&
         (t256 >= 4L * h->ncu || ((role == R_OUT || role == R_PROJ) && t256 >= 2L * h->ncu))) {
-        variant = epi == EPI_GELU ? 8 : 80;
+        variant = 8;
         const int lv = role == R_QKV ? h->large_var[0] : role == R_FC ? h->large_var[1]
                      : role == R_OUT ? h->large_var[2] : role == R_PROJ ? h->large_var[3] : 0;
         if (lv && (epi == EPI_STORE || epi == EPI_GELU)) {
@@ -1184,9 +1184,9 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 2;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
-    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 80, 62, 63, 72, 74)
+    else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 62, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
-        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 80 || m[0] == 62 || m[0] == 63 || m[0] == 72 || m[0] == 74);
+        ok = parse_list(v, m, 2) && (m[0] == 8 || m[0] == 62 || m[0] == 72 || m[0] == 74);
         if (ok) { h->split_main = m[0]; h->split_tail = m[1]; }
     } else if (k == "tail_variant") ok = parse_int(v, h->tail_var);
     else if (k == "tail_kmin") ok = parse_int(v, h->tail_kmin) && h->tail_kmin >= 64 && h->tail_kmin % 64 == 0;
@@ -1685,10 +1685,10 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     a.xcd_n = variant / 100;  // variant = 100 * xcd_partition + tile variant
     variant %= 100;
     int rc;
-    // 16-bit-output-only variants (80-82, 98 LDS-staged; 62 / 63 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
+    // 16-bit-output-only variants (81 / 82 / 98 LDS-staged; 62, 72-77 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
-    const bool staged = variant == 80 || variant == 81 || variant == 82 || variant == 98 || variant == 62 ||
-                        variant == 63 || variant == 72 || variant == 74 || variant == 75 || variant == 77;
+    const bool staged = variant == 81 || variant == 82 || variant == 98 || variant == 62 || variant == 72 ||
+                        variant == 74 || variant == 75 || variant == 77;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

@@ -853,9 +853,6 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
             if (a.N % 128) return -1;
             return launch_pipe<T, 160, 128, 2, 2, 2>(s, epi, a);
         // ---- LDS-staged row-contiguous 16-bit epilogue (SM = 3) ----
-        case 80:  // 256x256: every role of the large-M shapes (B/16, L/14)
-            if (a.N % 256) return -1;
-            return launch_pipe<T, 256, 256, 2, 4, 2, 3>(s, epi, a);
         case 81:  // 128x128: tail launch of the c_fc round split
             if (a.N % 128) return -1;
             return launch_pipe<T, 128, 128, 4, 2, 2, 3>(s, epi, a);
@@ -875,14 +872,14 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (a.blk_a || a.blk_c) {  // blocked u: pipelined 8..98 and persistent 62 / 63 / 72 / 74 / 75 / 77 only
+    if (a.blk_a || a.blk_c) {  // blocked u / h: pipelined 8..98 and persistent 62 / 72 / 74 / 75 / 77 only
         if (variant < 8 || a.ksplit > 1) return -1;
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
-    // blocked W: the pipelined tiles and the persistent tiles (62 / 63 / 72 / 74)
+    // blocked W: the pipelined tiles and the persistent tiles (62 / 72 / 74 / 75 / 77)
     if (a.blk_w && (variant < 8 || a.ksplit > 1)) return -1;
-    if (variant == 62 || variant == 63 || variant == 72 || variant == 74 || variant == 75 || variant == 77)
+    if (variant == 62 || variant == 72 || variant == 74 || variant == 75 || variant == 77)
         return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

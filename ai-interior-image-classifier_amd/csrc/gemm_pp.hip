@@ -363,7 +363,6 @@ static int launch_p32_320(hipStream_t s, int epi, const GemmArgs& a) {
 int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.N % 256 || a.K % 128 || a.K < 128 || a.ksplit > 1) return -1;
     if (a.N > 8192 || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
-    if (variant == 63) return dtype == 2 ? launch_ppp_t<F16, true>(s, epi, a) : launch_ppp_t<BF16, true>(s, epi, a);
     if (variant == 62) return dtype == 2 ? launch_ppp_t<F16, false>(s, epi, a) : launch_ppp_t<BF16, false>(s, epi, a);
     if (variant == 72 || variant == 74)
         return dtype == 2 ? launch_p32<F16>(s, epi, a, variant == 74) : launch_p32<BF16>(s, epi, a, variant == 74);

@@ -437,7 +437,7 @@ def test_lnfold_bs256_takes_the_single_launch(gpu, x24):
 
 
 # c_fc tile variants each row must reach (the launch log, tuning trace_gemm=1): 75 = the balanced
-# one-launch tile, 62 + 81 / 72 + 81 / 63 + 81 = round split main + tail, 22 = one launch on the
+# one-launch tile, 62 + 81 / 72 + 81 / 74 + 81 = round split main + tail, 22 = one launch on the
 # 160x128 tile, 74 / 8 = large-M tiles, 3 = the MX-fp8 persistent tile
 @pytest.mark.parametrize("name,dtype,B,tun,fc", [
     ("ViT-B/32", "fp16", 256, {}, [75]),        # c_fc: one balanced launch (default); c_proj v82
@@ -447,11 +447,11 @@ def test_lnfold_bs256_takes_the_single_launch(gpu, x24):
     ("ViT-B/32", "bf16", 67, {}, [22]),         # one launch per role
     ("ViT-B/32", "fp16", 1, {}, [22]),          # M = 50: the last 16-row block is padding
     ("ViT-B/32", "fp16", 256, {"lnfold": 1}, [22]),  # EPI_LNF_GELU c_fc, EPI_RES_STATS c_proj
-    ("ViT-B/32", "fp16", 256, {"split_variants": "63,81", "fc_balanced": 0}, [63, 81]),  # non-temporal main
+    ("ViT-B/32", "fp16", 256, {"split_variants": "74,81", "fc_balanced": 0}, [74, 81]),  # non-temporal main
     ("ViT-B/16", "fp16", 64, {}, [75]),         # N = 197: 600 tiles, balanced launch
     ("ViT-B/16", "fp16", 64, {"fc_balanced": 0}, [62, 81]),  # N = 197, round split
     ("ViT-L/14@336px", "fp16", 32, {}, [74]),   # large M: persistent v74 writes u, v72 reads it
-    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3463,80"}, [8]),  # v8 direct stores, v80 reads
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3462,8,3462,8"}, [8]),  # v8 direct stores, v62 / v8 read
     ("ViT-B/32", "mxfp8", 64, {}, [3, 22]),     # MX-fp8: fp8 u of the MX blocks, 16-bit u of the rest
     ("ViT-B/32", "mxfp8", 64, {"mx8_skip": ""}, [3]),  # every block MX; the last c_proj keeps u row-major
 ])
@@ -493,7 +493,7 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun, fc):
     ("ViT-B/16", "fp16", 256, {}, [74]),                      # large M: every role on 3472, c_fc 3474 (default)
     ("ViT-L/14@336px", "fp16", 32, {}, [74]),                 # large M: c_fc on the shipped 3474
     ("ViT-L/14@336px", "fp16", 64, {}, [74]),                 # every role large-M: 3472 / 3474, blocked A
-    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3463,80"}, [8]),  # large-M pipelined tiles
+    ("ViT-L/14@336px", "fp16", 32, {"large_variants": "3408,8,3462,8"}, [8]),  # large-M pipelined / ping-pong tiles
 ])
 def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun, fc):
     """The Linear weights read from their 16-row blocked copy (tuning w_blocked: 2 = every tile

@@ -804,6 +804,66 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    // p32x M N K epi xcd: the 320 x 256 form (BM = 320, variant 77's balanced grid) against the
+    // 256 x 256 one (variant 75), each with the ablation policies: which stream grows with BM
+    if (argc > 1 && std::string(argv[1]) == "p32x") {
+        const int M = atoi(argv[2]), N = atoi(argv[3]), K = atoi(argv[4]), epi = atoi(argv[5]), xcd = atoi(argv[6]);
+        u16 *A, *W, *C;
+        float* bias;
+        CK(hipMalloc(&A, (size_t)(M + 320) * K * 2));
+        CK(hipMalloc(&W, (size_t)N * K * 2));
+        CK(hipMalloc(&C, (size_t)M * N * 2));
+        CK(hipMalloc(&bias, (size_t)N * 4));
+        fill_f16<<<1024, 256>>>(A, (size_t)(M + 320) * K, 1);
+        fill_f16<<<1024, 256>>>(W, (size_t)N * K, 2);
+        CK(hipMemset(bias, 0, N * 4));
+        GemmArgs a{};
+        a.A = A; a.W = W; a.bias = bias; a.C = C;
+        a.M = M; a.N = N; a.K = K; a.ldc = N; a.xcd_n = xcd; a.blk_w = 1;
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        auto run = [&](const char* name, double tiles, auto fn) {
+            for (int i = 0; i < 5; ++i) fn();
+            float best = 1e9f;
+            for (int r = 0; r < 5; ++r) {
+                CK(hipEventRecord(e0));
+                for (int i = 0; i < 20; ++i) fn();
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                best = std::min(best, ms / 20);
+            }
+            printf("%-40s %7.2f us  %.0f TF/s  %.2f us per tile-round\n", name, best * 1e3,
+                   2.0 * M * N * K / (best * 1e-3) / 1e12, best * 1e3 / tiles);
+        };
+        for (int bm : {256, 320}) {
+            const int ntiles = ((M + bm - 1) / bm) * (N / 256), per = (ntiles + 255) / 256;
+            const int grid = (ntiles + per - 1) / per;
+            printf("BM %d: %d tiles on %d workgroups (%d per workgroup)\n", bm, ntiles, grid, per);
+#define P32X(NAME, BMV, HKT)                                                                               \
+    run(NAME, per, [&] {                                                                                    \
+        if (epi) gemm_p32_kernel<F16, EPI_GELU, false, true, false, BMV, HKT><<<grid, 512>>>(a, ntiles);  \
+        else gemm_p32_kernel<F16, EPI_STORE, false, true, false, BMV, HKT><<<grid, 512>>>(a, ntiles);     \
+    })
+            if (bm == 256) {
+                P32X("  BM 256 shipped", 256, P32Abl<0>);
+                P32X("  BM 256 no staging", 256, P32Abl<7>);
+                P32X("  BM 256 no MFMA", 256, P32Abl<8>);
+                P32X("  BM 256 no fragment reads", 256, P32Abl<9>);
+                P32X("  BM 256 no epilogue stores", 256, P32Abl<3>);
+            } else {
+                P32X("  BM 320 shipped", 320, P32Abl<0>);
+                P32X("  BM 320 no staging", 320, P32Abl<7>);
+                P32X("  BM 320 no MFMA", 320, P32Abl<8>);
+                P32X("  BM 320 no fragment reads", 320, P32Abl<9>);
+                P32X("  BM 320 no epilogue stores", 320, P32Abl<3>);
+            }
+#undef P32X
+        }
+        return 0;
+    }
     if (argc < 6) {
         fprintf(stderr, "usage: gemm_probe M N K epi xcd [iters] [grid]\n");
         return 2;

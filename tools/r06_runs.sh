@@ -97,6 +97,22 @@ run_ablk() {
   cat $out/ab.log
 }
 
+# kernel-level tile sweep of the N = 768 roles and QKV at B/32 bs 256 (blocked W; c_proj's A is the
+# blocked u: + 30000)
+run_tiles() {
+  out=gpurun_out/r06_tiles
+  mkdir -p $out
+  timeout -k 10 600 python -u tools/gemm_ab.py "12800,768,768,0" "10082,10081,10022,10080,10098,10008,13472,13475,13462" 5 20 \
+    > $out/out.log 2>&1 || { echo "out_proj sweep failed"; tail -10 $out/out.log; exit 1; }
+  cat $out/out.log
+  timeout -k 10 600 python -u tools/gemm_ab.py "12800,768,3072,0" "30082,30081,30022,30080,30098,33472,33475,33462" 5 20 \
+    > $out/proj.log 2>&1 || { echo "c_proj sweep failed"; tail -10 $out/proj.log; exit 1; }
+  cat $out/proj.log
+  timeout -k 10 600 python -u tools/gemm_ab.py "12800,2304,768,0" "10298,10098,10082,10022,13472,13475,13462,10080" 5 20 \
+    > $out/qkv.log 2>&1 || { echo "qkv sweep failed"; tail -10 $out/qkv.log; exit 1; }
+  cat $out/qkv.log
+}
+
 recipe=${1:-}
 shift || true
 case "$recipe" in
@@ -106,5 +122,6 @@ case "$recipe" in
   t320) run_t320 "$@" ;;
   phases) run_phases "$@" ;;
   ablk) run_ablk "$@" ;;
+  tiles) run_tiles "$@" ;;
   *) echo "recipes: check | tests <expr> [files] | ab '<bench args>' R arm..."; exit 2 ;;
 esac
