@@ -28,7 +28,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", f"-I{CSRC}",
           "-mllvm", "--amdgpu-mfma-vgpr-form", "-Wno-unused-result", "-Wno-unused-value"]
 # Per-source flags. gemm.hip: the max-memory-clause machine scheduler (clusters each k-step's
-# staging loads). Same-box A/B of the two builds: B/32 +0.2 / +0.6 %, B/16
+# staging loads). Same-box A/B of the two builds (profiles/design_r05.md §11): B/32 +0.2 / +0.6 %, B/16
 # +0.5 %, L/14@336 +0.7 / +1.0 % img/s, patch GEMM -7 %; on attention.hip it cost 6 %, so
 # only the GEMMs get it.
 SRC_FLAGS = {"gemm": ["-mllvm", "--amdgpu-sched-strategy=max-memory-clause"]}

@@ -28,7 +28,7 @@ class ViTConfig:
         return self.grid * self.grid + 1
 
     def gflop_per_image(self) -> float:
-        """Algorithmic GFLOP per image (DESIGN.md §Measurement): GEMMs 2MNK, attention 4 N^2 D
+        """Algorithmic GFLOP per image (DESIGN.md §7): GEMMs 2MNK, attention 4 N^2 D
         per layer; LayerNorm/softmax/GELU not counted; merged LoRA adds 0."""
         N, D, G2 = self.tokens, self.width, self.grid ** 2
         patch = 2.0 * G2 * (3 * self.patch_size ** 2) * D

@@ -431,7 +431,7 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
 
 // kernel choice by sequence length: attention_v3 (two query fragments per wave) for N > 128,
 // attention_v2 for N <= 128 (one key block at N <= 64: ViT-B/32's N = 50) and for the causal
-// text tower. Two query fragments per wave at N <= 64 measured slower.
+// text tower (profiles/design_r05.md §11). Two query fragments per wave at N <= 64 measured slower.
 
 // attention with the output quantized to MX-fp8 (q8 [B N, D] e4m3 + q8s [B N, D / 32] scales) in
 // the kernel, for the shapes that run on the one-key-block attention_v2 (N <= 64: ViT-B/32);

@@ -86,7 +86,7 @@ struct Lane {
 // A workspace slot serves one call at a time. A batch of B >= SPLIT_MIN images runs as two
 // independent halves on the two lane streams (forked from / joined into the caller's stream
 // by events), so one half's memory-bound kernels and GEMM tails overlap the other half's
-// GEMMs (DESIGN.md §Streams). Smaller batches run on the caller's stream with lane 0.
+// GEMMs (DESIGN.md §5.5). Smaller batches run on the caller's stream with lane 0.
 constexpr int kLanes = 2;
 // Default: split batches of at least SPLIT_IMAGES images and SPLIT_TOKENS tokens (B/32: 512
 // images; B/16 and L/14@336: 130 / 128). B/32 at bs 256 stays on one stream: there the split
@@ -161,7 +161,7 @@ struct clipvit_handle {
     // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
     // tile; 0 = the 2-phase 256x256 tile (8). Default: the persistent ping-pong tile with the
     // column-group-major map (3462, gemm_pp.hip): B/16 22.3k -> 23.0k img/s, L/14@336 2,322 ->
-    // 2,388 (same-box A/B); c_fc with non-temporal output stores (3463): its
+    // 2,388 (same-box A/B, profiles/design_r05.md §5.8); c_fc with non-temporal output stores (3463): its
     // family 7.49 -> 7.03 ms per L/14 lane forward; out_proj / c_proj on 3463 too: L/14@336
     // 2,392-2,396 -> 2,416 img/s (B/16 unchanged). r05: the 32-deep-k-step tile (3472, gemm_p32.h)
     // on every role with QKV / c_fc reading their blocked weight copies (w_blk): L/14@336 bs 128
@@ -196,7 +196,7 @@ struct clipvit_handle {
     int mx8_split_tail = 0;
     // blocks kept in bf16 in MX-fp8 mode (bit i = block i); default the first two and last two
     // (measured: config-5 logit deviation 2.0e-2 with every block MX-fp8, 1.7e-2 with these
-    // four in bf16 — DESIGN.md §MX-fp8); tuning mx8_skip="..." overrides
+    // four in bf16 — DESIGN.md §5.6); tuning mx8_skip="..." overrides
     uint64_t mx8_skip = 0;
     // blocks whose MLP (c_fc, c_proj) stays bf16: the attention roles (QKV, out_proj) follow
     // mx8_skip, the MLP roles this mask (tuning mx8_skip sets both, mx8_skip_mlp this one):
@@ -210,7 +210,7 @@ struct clipvit_handle {
     bool resid16 = false;
     // deferred residual store (fp16 path, see forward()); tuning defer_x=0 disables
     bool defer_x = true;
-    // LayerNorm fold (tuning lnfold=1, fp16 only; DESIGN.md §LayerNorm): ln_1 / ln_2
+    // LayerNorm fold (tuning lnfold=1, fp16 only; DESIGN.md §5.1): ln_1 / ln_2
     // become per-row statistics written by the residual producers' epilogues (out_proj, c_proj,
     // embedding) and an affine correction in the QKV / c_fc epilogues; no LayerNorm pass
     bool lnfold = false;
@@ -703,7 +703,7 @@ static int cls_tail(clipvit_handle* h, hipStream_t s, int B, Lane* w, float* f_o
     return 0;
 }
 
-// MX-fp8 encoder forward (same sequence as forward(); see DESIGN.md §MX-fp8). Blocks listed in
+// MX-fp8 encoder forward (same sequence as forward(); see DESIGN.md §5.6). Blocks listed in
 // mx8_skip run the 16-bit path; every LayerNorm writes the format its consumer block uses.
 // resid16 (default): out_proj / c_proj store their bf16 branch outputs y, y2 in the dead qkv
 // buffer and the deferred add + LayerNorm kernels do the fp32 residual adds, as in forward().
@@ -839,7 +839,7 @@ static int cls_tail_fold(clipvit_handle* h, hipStream_t s, int B, Lane* w, float
     return 0;
 }
 
-// Encoder forward with the LayerNorm fold (DESIGN.md §LayerNorm). Buffers: x fp32 residual;
+// Encoder forward with the LayerNorm fold (DESIGN.md §5.1). Buffers: x fp32 residual;
 // x16 = 16-bit copy of x (the A operand of QKV in h, of c_fc in the dead qkv buffer); st = the
 // per-row 128-column statistics of x. Per block:
 //   QKV   = EPI_LNF(x16 (h), W_qkv diag(ln_1.g))        -> qkv        [ln_1 folded]
@@ -1102,7 +1102,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out) 
     // 16-bit residual branch outputs for both 16-bit types (bf16 too since r02: measured 76.3k ->
     // 78.9k img/s at bs 256 with the logit error unchanged, 4.35e-3 -> 4.13e-3)
     h->resid16 = true;  // fp16, bf16 and MX-fp8 (its bf16 branch outputs)
-    // off by default: measured slower (DESIGN.md §LayerNorm: the residual epilogues run in lockstep
+    // off by default: measured slower (DESIGN.md §5.1: the residual epilogues run in lockstep
     // at the end of one-round GEMMs; B/32 78.2k -> 74.3k img/s, B/16 20.6k -> 19.2k, L/14 2116 -> 2008)
     h->lnfold = false;
     h->split_min = std::max(SPLIT_IMAGES, (SPLIT_TOKENS + h->N - 1) / h->N);

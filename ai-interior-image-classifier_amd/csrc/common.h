@@ -137,7 +137,7 @@ enum Epi {
     EPI_F32GELU = 5, // C (f32) = quickgelu(acc + bias)              (tests)
     EPI_GELU_Q8 = 7, // C (MX-fp8) = quickgelu(acc + bias), block scales to sC  (MX-fp8 GEMM)
     EPI_Q8 = 8,      // C (MX-fp8) = acc + bias, block scales to sC             (tests)
-    // LayerNorm folded into the consumer GEMM (DESIGN.md §LayerNorm): A = fp16(x) (the residual
+    // LayerNorm folded into the consumer GEMM (DESIGN.md §5.1): A = fp16(x) (the residual
     // stream, NOT normalised), W' = W diag(gamma); per row mu / rstd from the producer's
     // 128-column partial statistics st_in; bias = b' = b + W beta, lnf_s = s_n = sum_k W'_nk:
     EPI_LNF = 9,       // C (T) = rstd (acc - mu s_n) + b'_n                  = LN(x) W^T + b

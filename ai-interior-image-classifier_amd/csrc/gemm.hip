@@ -7,7 +7,7 @@
 // mlp.c_proj.weight; conv1.weight viewed as [width, 3*p*p]).  Both operands are K-major, so
 // every MFMA fragment is one 16-byte LDS read.
 //
-// Design (DESIGN.md §Kernels/GEMM):
+// Design (DESIGN.md §5):
 //  * block tile BM x BN x 64, waves arranged WM x WN, each wave TM x TN = (BM/WM) x (BN/WN);
 //  * global -> LDS by global_load_lds_dwordx4 (no VGPR staging), two LDS buffers, next tile's
 //    loads issued before the current tile's MFMAs;

@@ -6,7 +6,7 @@
 //
 // Same operand conventions as gemm.hip (K-major A and packed W, swapped MFMA operands so a lane
 // owns one token and 16 contiguous features, LDS rows of 128 B with 16-B chunk c of row r at
-// c ^ (r & 7)), different schedule:
+// c ^ (r & 7)), different schedule (profiles/design_r05.md §5.8):
 //
 //  * waves 0-3 (group 0) and 4-7 (group 1) each own 128 token rows x 64 features per wave
 //    (wave w: rows 128 (w >> 2) .., features 64 (w & 3) ..); each SIMD hosts one wave of each

@@ -417,7 +417,7 @@ static int launch_mx8_tile(hipStream_t s, int epi, const GemmArgs& a) {
 
 // ---------------------------------------------------------------------------------------
 // Ping-pong MX-fp8 tile (variant 3, persistent): gemm_ppp_kernel's
-// schedule (gemm_pp.hip) at BK = 128 fp8. A k-tile row is 128 B in both
+// schedule (gemm_pp.hip, profiles/design_r05.md §5.8) at BK = 128 fp8. A k-tile row is 128 B in both
 // formats, so the LDS layout, the staging pieces and the phase/slot plan are the 16-bit
 // kernel's; per phase a wave runs 8 scaled 16x16x128 MFMAs (2x the cycles of the 16-bit form,
 // so the same matrix-pipe time per phase as the 16 bf16 MFMAs it replaces). Each stage also

@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(float* __restrict__ x, vo
 }
 
 // ---------------------------------------------------------------------------------------
-// LayerNorm fold (DESIGN.md §LayerNorm). Per row: the (mean, M2) of every 128-column group
+// LayerNorm fold (DESIGN.md §5.1). Per row: the (mean, M2) of every 128-column group
 // (lanes 0-31 hold group 2i of the float4 slice i, lanes 32-63 group 2i + 1): sum over the 32
 // lanes, mean, then the squared deviations from it (two-pass), lanes 0 / 32 write.
 template <int V>

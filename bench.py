@@ -415,7 +415,7 @@ def main():
     achieved = mlp_flop / (fc_ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[a.dtype]
     # FLOPs executed per image: the last block's out_proj/MLP run on the class token only
-    # (dead-row elimination, DESIGN.md §Last block), so those N-1 rows are not counted
+    # (dead-row elimination, DESIGN.md §5, class-token tail), so those N-1 rows are not counted
     pruned = 2.0 * (N - 1) * D * 9 * D / 1e9 if fam.get("cls_tail", 0.0) > 0 else 0.0
     gflop_img = cfg.gflop_per_image() - pruned
     model_tflops = value / world * gflop_img / 1e3

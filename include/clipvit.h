@@ -212,7 +212,7 @@ int clipvit_text_destroy(clipvit_text_handle* h);
  * main.py:489 for images already decoded to RGB (load_image, main.py:119-128):
  * Resize(n_px, BICUBIC) -> CenterCrop(n_px) -> ToTensor -> Normalize(CLIP mean/std).
  * The resampling is Pillow's 8-bit fixed-point two-pass convolution, bit-identical to
- * PIL.Image.resize(BICUBIC) followed by the crop (DESIGN.md §Preprocessing). */
+ * PIL.Image.resize(BICUBIC) followed by the crop (DESIGN.md §9). */
 typedef struct {
     int64_t offset;   /* byte offset of the image's HWC uint8 RGB pixels in rgb_dev */
     int width;        /* source width  (pixels) */
@@ -244,7 +244,7 @@ int clipvit_resample_plan(int in_size, int out_size, int* ksize, int* bounds, in
  * 20 + S = split-K into S slices (pipelined variants >= 8; C holds [S][M][N] fp32 partial
  * products without bias; K % (64 S) == 0 — the class-token tail's GEMMs). K % 64 == 0, N % 64 == 0 (N % 128 for variants 1-2,
  * N % 256 for variant 3). variant % 100 selects the tile kernel (0 auto; the table in
- * csrc/gemm.hip pick/launch_gemm, DESIGN.md §GEMM); variant / 100 the block->XCD mapping
+ * csrc/gemm.hip pick/launch_gemm, DESIGN.md §5.2); variant / 100 the block->XCD mapping
  * (0/1 = 1-D bijective remap, 2 = 4x2 (M-band, N-half) partition; pipelined variants only);
  * + 10000 = W in the 16-row blocked layout, + 20000 = A blocked, + 30000 = both.
  * The same encoding applies to clipvit_gemm_bench. */
@@ -273,7 +273,7 @@ int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsig
                           const float* W_dev, const float* bias_dev, void* C_dev,
                           unsigned char* sC_dev, int M, int N, int K, int epi, int variant);
 
-/* The 24-bit residual stream format of the 16-bit forward (DESIGN.md §0): x fp32 [n] (n % 4 == 0)
+/* The 24-bit residual stream format of the 16-bit forward (DESIGN.md §3): x fp32 [n] (n % 4 == 0)
  * -> planes [3n bytes: n u16 upper halves, then n bytes of the next 8 mantissa bits, rounded to
  * nearest at bit 8] -> back fp32 [n], by the kernels' own encode / decode functions. */
 int clipvit_residual_x24_test(void* stream, const float* x_dev, void* planes_dev, float* back_dev, size_t n);

@@ -1,4 +1,4 @@
-"""CPU precision study of the vision tower's number formats (test infrastructure; DESIGN.md §3, §5.5).
+"""CPU precision study of the vision tower's number formats (test infrastructure; DESIGN.md §3).
 
 Runs the oracle's ViT forward (oracle/clip_ref.py, fp32) with chosen tensors rounded to 16 bits
 and reports the bench's parity metric (per image max|dlogit| / max|logit_ref|) and the feature

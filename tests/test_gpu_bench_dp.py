@@ -5,7 +5,7 @@ both ranks' images, and the rehearsal is labelled as such (n_gpus 1, ranks 2, no
 point), and the line reports what the collective did: the world size the process group saw, its
 backend, and gather_ok (rank 0's slice of the gathered logits equals its local logits bit for
 bit, checked once after the timed loop). On the driver's N-GPU runs the backend is nccl (RCCL);
-here it is gloo. The RCCL calls themselves are checked by tools/rccl_check.py (DESIGN.md §7)."""
+here it is gloo. The RCCL calls themselves are checked by tools/rccl_check.py (DESIGN.md §6)."""
 import json
 import os
 import subprocess

@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 # 1e-3 relative is the BASELINE bar; fp16 operands (the default, and the reference's own CUDA
 # dtype) meet it in every config. bf16 (8-bit mantissa) does NOT: measured ~1.4e-3 at realistic
 # logit scale and ~4.4e-3 against random text rows, so its checks use the looser bounds below
-# (DESIGN.md §Precision).
+# (DESIGN.md §3).
 LOGIT_TOL = {("bf16", "peaked"): 2e-3, ("fp16", "peaked"): 1e-3,
              ("bf16", "random"): 6e-3, ("fp16", "random"): 1e-3}
 PROB_TOL = {"bf16": 2e-2, "fp16": 5e-3}

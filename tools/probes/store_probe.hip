@@ -1,4 +1,4 @@
-// Epilogue-store probe: how fast can 256 workgroups (one per CU, 8 waves) write
+// Epilogue-store probe (profiles/design_r05.md §5.8): how fast can 256 workgroups (one per CU, 8 waves) write
 // 16-bit 256x256 output tiles, by lane->address pattern? Same bytes in every arm.
 //
 //   frag : the ping-pong GEMM's pattern: for fm in 0..7 a wave stores rows (16 per fm) x 64 features,
