@@ -113,6 +113,26 @@ run_tiles() {
   cat $out/qkv.log
 }
 
+# the round's profile (tools/profile_round.sh: kernel trace + FETCH / WRITE / MFMA / L2 passes,
+# then the default bench with its PMC traffic) and the other configurations' bench lines
+run_closing() {
+  out=gpurun_out/r06_closing
+  mkdir -p $out
+  timeout -k 10 1100 bash tools/profile_round.sh gpurun_out/prof_r06 r06 > $out/profile.log 2>&1 \
+    || { echo "profile round failed"; tail -20 $out/profile.log; exit 1; }
+  tail -2 $out/profile.log
+  for c in "cfg4|--model ViT-L/14@336px --batch 128 --lora-rank 16 --steps 5 --warmup 2" \
+           "b16|--model ViT-B/16 --steps 10 --warmup 3" \
+           "b32_bf16|--dtype bf16 --steps 20 --warmup 5" \
+           "cfg5_mx|--dtype mxfp8 --batch 512 --steps 20 --warmup 5" \
+           "cfg5_bf16|--dtype bf16 --batch 512 --steps 20 --warmup 5 --no-cpu-baseline"; do
+    name=${c%%|*}; args=${c#*|}
+    timeout -k 10 300 python bench.py $args > $out/$name.json 2> $out/$name.err \
+      || { echo "bench $name failed"; tail -10 $out/$name.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$out/$name.json'));print('$name', d['value'], d['ms_per_step'], d.get('parity'))"
+  done
+}
+
 recipe=${1:-}
 shift || true
 case "$recipe" in
@@ -123,5 +143,6 @@ case "$recipe" in
   phases) run_phases "$@" ;;
   ablk) run_ablk "$@" ;;
   tiles) run_tiles "$@" ;;
+  closing) run_closing "$@" ;;
   *) echo "recipes: check | tests <expr> [files] | ab '<bench args>' R arm..."; exit 2 ;;
 esac
