@@ -58,6 +58,23 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
 // row-swap permutes (VALU; __shfl_xor is an LDS ds_bpermute round trip). Each swap exchanges
 // rows between its two operands; max of the two results is max(v[l], v[l ^ 16]) (resp. ^ 32)
 // in every lane, whichever operand received which half.
+// CLIP's QuickGELU x sigmoid(1.702 x) = x / (1 + 2^(-1.702 log2(e) x)): one multiply by the folded
+// constant, v_exp_f32, an add, v_rcp_f32 and the final multiply. Every GEMM epilogue and the
+// split-K tail call this one function, so every tile's c_fc output is the same bits.
+__device__ __forceinline__ float quick_gelu(float x) {
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-2.4554669595930157f * x));
+}
+// the same on two values (bit-identical): the multiplies and the add as v_pk_*_f32
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void quick_gelu2(float& a, float& b) {
+    const f32x2 y = {a, b};
+    const f32x2 z = y * (f32x2){-2.4554669595930157f, -2.4554669595930157f};
+    const f32x2 d = (f32x2){__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + (f32x2){1.0f, 1.0f};
+    const f32x2 o = y * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    a = o.x;
+    b = o.y;
+}
+
 __device__ __forceinline__ float max_rows4(float v) {
     const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
     v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));

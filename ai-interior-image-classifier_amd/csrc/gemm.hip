@@ -140,7 +140,7 @@ __global__ __launch_bounds__(64 * WM* WN) void gemm_nt_kernel(GemmArgs a) {
             }
             if constexpr (EPI == EPI_GELU || EPI == EPI_F32GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] = quick_gelu(v[i]);
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU) {
                 uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                 else colv_add(v, colv + nl);
                 if constexpr (GELU) {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                    for (int i = 0; i < 16; ++i) v[i] = quick_gelu(v[i]);
                 }
                 const int c0 = nl >> 3;  // 16-B chunk of the row
                 unsigned char* rowp = smem + r * ROWB;
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
             }
             if constexpr (GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] = quick_gelu(v[i]);
             }
             if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || LNF) {
                 // blocked C: n % 16 == 0, so n + 8 is the next chunk of the same 64-block (+256 B)

@@ -22,7 +22,7 @@
 //  * the epilogue (bias + QuickGELU for c_fc + conversion + stores) runs in the wave's first read
 //    segment of the next tile, after that segment's staging issue; its stores are younger than
 //    the staged pieces the next waits count, which allow for them. Its arithmetic is variant
-//    62's / the pipelined tiles' (acc from 0, + bias, x / (1 + __expf(-1.702 x))), so every tile
+//    62's / the pipelined tiles' (acc from 0, + bias, quick_gelu in common.h), so every tile
 //    gives the same bits and the tile choice (per shape, per lane split) never changes a result.
 //
 // Schedule. Slot = barrier interval. Group g's read segment of k-step t is slot 2t + g, its MFMA
@@ -226,11 +226,14 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 #pragma unroll
             for (int f = 0; f < 4; ++f)
 #pragma unroll
-                for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
+                for (int rr = 0; rr < 4; rr += 2) {  // v_pk_add_f32
+                    const f32x2 s = (f32x2){acc[f][fm][rr], acc[f][fm][rr + 1]} + (f32x2){bv[f][rr], bv[f][rr + 1]};
+                    v[4 * f + rr] = s.x;
+                    v[4 * f + rr + 1] = s.y;
+                }
             if constexpr (GELU) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x), as variant 62 / the pipelined tiles
-                    v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                for (int q = 0; q < 16; q += 2) quick_gelu2(v[q], v[q + 1]);  // x sigmoid(1.702 x)
             }
             u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
             u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};

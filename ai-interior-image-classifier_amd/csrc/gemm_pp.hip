@@ -267,7 +267,7 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
                 for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
             if constexpr (GELU) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                for (int q = 0; q < 16; ++q) v[q] = quick_gelu(v[q]);
             }
             if (m < a.M) {
                 // blocked C (blk_c): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes

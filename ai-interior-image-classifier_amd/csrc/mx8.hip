@@ -352,7 +352,7 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
             }
             if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_F32GELU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) v[i] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[i]));
+                for (int i = 0; i < 16; ++i) v[i] = quick_gelu(v[i]);
             }
             if constexpr (EPI == EPI_GELU_Q8 || EPI == EPI_Q8) {
                 // MX block = 32 features = this lane's 16 + those of lane ^ 16 (same token)
@@ -716,7 +716,7 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                 for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
             if constexpr (EPI == EPI_GELU_Q8) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                for (int q = 0; q < 16; ++q) v[q] = quick_gelu(v[q]);
                 // MX block = 32 features = this lane's 16 + those of lane ^ 16 (same token):
                 // ds_swizzle bitmask mode, xor 0x10 within 32-lane groups (no address VGPR)
                 float am = 0.f;

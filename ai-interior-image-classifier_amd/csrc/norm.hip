@@ -476,7 +476,7 @@ __global__ __launch_bounds__(256) void splitk_gelu_kernel(const float* __restric
     const float4 bb = *(const float4*)(bias + e % n);
     float v[4] = {t.x + bb.x, t.y + bb.y, t.z + bb.z, t.w + bb.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[k]));
+    for (int k = 0; k < 4; ++k) v[k] = quick_gelu(v[k]);
     *(uint2*)(u + e) = make_uint2(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]));
 }
 

@@ -284,7 +284,7 @@ __global__ __launch_bounds__(512, 1) void ppp_probe(GemmArgs a, int ntiles, unsi
                 for (int rr = 0; rr < 4; ++rr) v[4 * f + rr] = acc[f][fm][rr] + bv[f][rr];
             if constexpr (GELU) {
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                for (int q = 0; q < 16; ++q) v[q] = quick_gelu(v[q]);
             }
             const bool live = ABL == 3 ? (m < a.M && a.ldc > (1 << 30)) : m < a.M;
             if (live) {

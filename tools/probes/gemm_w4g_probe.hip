@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256, 1) void gemm_w4_kernel(GemmArgs a, int ntiles)
                 if constexpr (GELU) {
 #pragma unroll
                     for (int q = 0; q < 16; ++q)  // x sigmoid(1.702 x), as gemm_p32.h
-                        v[q] *= __builtin_amdgcn_rcpf(1.0f + __expf(-1.702f * v[q]));
+                        v[q] = quick_gelu(v[q]);
                 }
                 u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
                 u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
