@@ -133,6 +133,7 @@ struct clipvit_handle {
     std::unordered_map<std::string, std::vector<int64_t>> shapes;
     std::vector<std::string> order;
     void* wpatch = nullptr;
+    void* wpatch_b = nullptr;  // its 16-row blocked copy (the explicit patch GEMM, patch_im2col)
     std::vector<LayerW> layers;
     float* scratch = nullptr;
     size_t scratch_elems = 0;
@@ -281,6 +282,10 @@ struct clipvit_handle {
     // LayerNorm +0.018), 83.08-83.48k with 1 (profiles/r06/hblk_inmodel_ab.txt). QKV's h stays
     // row-major: its 240x256 tile measured the same either way (profiles/r06/hblk_v1_inmodel_ab.txt)
     int h_blk = 2;
+    // patch embedding as blocked im2col (the pixel cast writes the GEMM's A in the 16-row blocked
+    // layout) + the pipelined 160x128 tile on blocked A and W, instead of the implicit GEMM over
+    // the cast pixels (tuning patch_im2col; only where a cast pass runs anyway)
+    int patch_im2col = 1;
     int use_hblk() const { return use_x24() && !lnfold ? h_blk : 0; }
     // test hook (tuning trace_gemm=1): every role GEMM launch of gemm() / gemm8() appends
     // {role, tile variant, M, flags} here (clipvit_gemm_log), so a test can assert which kernel
@@ -570,6 +575,26 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
 // feed the patch tiles directly; other input dtypes are cast once into the u buffer.
 static int patch_embed(clipvit_handle* h, hipStream_t s, const void* pix, int in_dtype, int B, Lane* w) {
     const int R = h->cfg.image_size, P = h->cfg.patch_size;
+    if (h->patch_im2col && (P % 8 || in_dtype != h->dt) && h->Kp <= 4 * h->D) {
+        // blocked im2col into u ([B G^2 rows padded to 16, Kp] <= u's [B N, 4 D]), then the
+        // pipelined 160x128 tile (v22) on blocked A and W; same k order and k-tile sequence as
+        // the implicit GEMM below
+        if (launch_im2col_blk(s, in_dtype, h->dt, pix, w->u, B, R, P, h->Kp) != 0) {
+            g_err = "patch embedding: unsupported patch size for im2col";
+            return CLIPVIT_E_INVALID;
+        }
+        GemmArgs a{};
+        a.A = w->u; a.W = h->wpatch_b; a.bias = nullptr; a.C = w->x;
+        a.M = B * h->G2; a.N = h->D; a.K = h->Kp; a.ldc = h->D;
+        a.patch_g2 = h->G2; a.patch_ntok = h->N;
+        a.xcd_n = h->xcd[R_PATCH];
+        a.blk_a = 1; a.blk_w = 1;
+        if (launch_gemm(s, h->dt, EPI_PATCH, a, 22) != 0) {
+            g_err = "patch embedding: explicit patch GEMM refused the shape";
+            return CLIPVIT_E_INVALID;
+        }
+        return 0;
+    }
     const void* px16 = pix;
     int Rw = R;
     if (P % 8) {  // P = 14: patch rows padded to 16 pixels (aligned 16-byte chunks)
@@ -1183,6 +1208,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 2;
+    else if (k == "patch_im2col") ok = parse_int(v, h->patch_im2col) && (h->patch_im2col == 0 || h->patch_im2col == 1);
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 62, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
@@ -1244,13 +1270,13 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
-        int h_blk, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int h_blk, patch_im2col, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1266,7 +1292,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1327,6 +1353,7 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
         return hipMalloc(&p, elems * 2);
     };
     HIPCHK(alloc16(h->wpatch, D * h->Kp));
+    HIPCHK(alloc16(h->wpatch_b, D * h->Kp));
     h->layers.resize(h->cfg.layers);
     size_t maxw = D * h->K3;
     // blocked weight copies of the Linears that pack_linear re-lays out: not for the MX-fp8 roles
@@ -1372,6 +1399,7 @@ int clipvit_load_weights(clipvit_handle* h, const clipvit_tensor* tensors, size_
     hipStream_t s = nullptr;
     launch_patch_weight_relayout(s, h->master["visual.conv1.weight"], h->scratch, (int)D, h->cfg.patch_size);
     launch_pack_weight(s, h->dt, h->scratch, h->wpatch, (int)D, h->K3, h->Kp);
+    launch_blk16_relayout(s, h->wpatch, h->wpatch_b, (int)D, h->Kp);
     for (int i = 0; i < h->cfg.layers; ++i) {
         LayerW& ly = h->layers[i];
         pack_linear(h, s, L(i, "attn.in_proj_weight"), ly.wqkv, nullptr);
@@ -1608,6 +1636,7 @@ int clipvit_destroy(clipvit_handle* h) {
     hipDeviceSynchronize();
     for (auto& kv : h->master) hipFree(kv.second);
     hipFree(h->wpatch);
+    hipFree(h->wpatch_b);
     for (auto& ly : h->layers) {
         hipFree(ly.wqkv);
         hipFree(ly.wout);

@@ -360,6 +360,10 @@ void launch_cast_pixels(hipStream_t s, int in_dtype, int out_dtype, const void* 
 // [B, 3, R, R] -> [B, 3, R, G * 16] 16-bit with every P-pixel patch row padded to 16 (zeros)
 void launch_cast_pixels_padded(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B,
                                int R, int P);
+// pixels [B, 3, R, R] -> the explicit patch GEMM's A: [roundup16(B G^2), Kp] 16-bit, 16-row blocked
+// (blk16_off), k in the implicit patch GEMM's order; -1 on an unsupported P / Kp
+int launch_im2col_blk(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B, int R, int P,
+                      int Kp);
 // conv1.weight [D, 3, P, P] fp32 -> [D, 3 * P * roundup8(P)] in the implicit patch GEMM's k order
 void launch_patch_weight_relayout(hipStream_t s, const float* w, float* out, int D, int P);
 

@@ -111,6 +111,66 @@ void launch_cast_pixels(hipStream_t s, int in_dtype, int out_dtype, const void* 
     else cast_dispatch<BF16>(s, in_dtype, src, dst, n);
 }
 
+// Blocked im2col for the explicit patch GEMM (tuning patch_im2col): pixels [B, 3, R, R] of any
+// dtype -> A [Mp, Kp] 16-bit in the 16-row blocked layout (blk16_off), row m = patch
+// (b, py, px) of the GEMM (m = b G^2 + py G + px), k in the implicit patch GEMM's order
+// (patch_koff: k = c P PP + r PP + j, PP = P rounded up to 8, zero at j >= P and k >= 3 P PP),
+// rows m >= M zero. One thread per 16-byte chunk (8 pixels of one patch row), numbered in
+// output order: a wave writes 1 KB contiguous (4 chunks x 16 rows of a 2 KB block), and the
+// 4 lanes of one row and pixel row read its 4 x 8 pixels = one contiguous 32-pixel run.
+template <typename TO, int IN, int P>
+__global__ void im2col_blk_kernel(const void* __restrict__ src, u16* __restrict__ dst, int M, int Mp, int Kp,
+                                  int R) {
+    constexpr int PP = (P + 7) / 8 * 8, CH = P * PP;
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int kb = Kp >> 6;
+    if (i >= (long)(Mp >> 4) * kb * 128) return;
+    const int row = (int)(i & 15), chunk = (int)((i >> 4) & 7);
+    const long blk = i >> 7;
+    const int mb = (int)(blk / kb), kt = (int)(blk % kb);
+    const int m = mb * 16 + row, k = kt * 64 + chunk * 8;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (m < M && k < 3 * CH) {
+        const int G = R / P, G2 = G * G;
+        const int b = m / G2, pp = m - b * G2, py = pp / G, px = pp - py * G;
+        const int c = k / CH, rem = k - c * CH, r = rem / PP, j0 = rem - r * PP;
+        const size_t base = (((size_t)b * 3 + c) * R + (size_t)py * P + r) * R + (size_t)px * P + j0;
+        if constexpr (IN == 0 && P % 8 == 0) {
+            const float4 a0 = *(const float4*)((const float*)src + base), a1 = *(const float4*)((const float*)src + base + 4);
+            v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
+            v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                if (j0 + e < P) v[e] = load_pix<IN>(src, base + e);
+        }
+    }
+    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                  pack2<TO>(v[6], v[7]));
+}
+
+template <typename TO, int IN>
+static int im2col_p(hipStream_t s, const void* src, void* dst, int M, int Mp, int Kp, int R, int P) {
+    const long n = (long)(Mp >> 4) * (Kp >> 6) * 128;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    switch (P) {
+        case 14: im2col_blk_kernel<TO, IN, 14><<<g, 256, 0, s>>>(src, (u16*)dst, M, Mp, Kp, R); return 0;
+        case 16: im2col_blk_kernel<TO, IN, 16><<<g, 256, 0, s>>>(src, (u16*)dst, M, Mp, Kp, R); return 0;
+        case 32: im2col_blk_kernel<TO, IN, 32><<<g, 256, 0, s>>>(src, (u16*)dst, M, Mp, Kp, R); return 0;
+    }
+    return -1;
+}
+
+int launch_im2col_blk(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B, int R, int P,
+                      int Kp) {
+    const int G = R / P, M = B * G * G, Mp = (M + 15) & ~15;
+    if (Kp % 64 || R % P) return -1;
+#define I2C(TO) (in_dtype == 0 ? im2col_p<TO, 0>(s, src, dst, M, Mp, Kp, R, P) \
+                 : in_dtype == 1 ? im2col_p<TO, 1>(s, src, dst, M, Mp, Kp, R, P) : im2col_p<TO, 2>(s, src, dst, M, Mp, Kp, R, P))
+    return out_dtype == 2 ? I2C(F16) : I2C(BF16);
+#undef I2C
+}
+
 // ---------------------------------------------------------------------------------------
 // Row LayerNorm helpers ln_row / store_row16: common.h (shared with text.hip).
 

@@ -105,7 +105,11 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
  * qkv_variant / fc_variant (100 * XCD map + tile of the QKV / c_fc role only); fc_balanced (0/1:
  * c_fc with >= 2 whole rounds of 256x256 tiles plus a remainder as one balanced launch, default 1,
- * or as the round split of split_variants); trace_gemm (0/1: clipvit_gemm_log);
+ * or as the round split of split_variants); fc_balanced_variant (75 / 77: its tile);
+ * h_blocked (0/1/2: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
+ * LDS transpose (2, default)); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
+ * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
+ * trace_gemm (0/1: clipvit_gemm_log);
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p"; mx8_skip / mx8_skip_mlp "i,j,.." (bf16
  * blocks; mx8_skip sets both masks). An unknown key or bad value fails with CLIPVIT_E_INVALID
  * and leaves the handle unchanged. The product path never calls it. */

@@ -559,3 +559,33 @@ def test_blocked_h_is_bit_identical(gpu, name, dtype, B, tun, hmode):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
+
+
+@pytest.mark.parametrize("name,dtype,B,pix16", [
+    ("ViT-B/32", "fp16", 256, False),   # fp32 pixels (the bench): cast pass -> blocked im2col
+    ("ViT-B/32", "bf16", 67, False),    # ragged M = 67 * 49: the last 16-row block is part padding
+    ("ViT-B/32", "fp16", 1, False),     # M = 49
+    ("ViT-B/16", "fp16", 130, False),   # two lanes, P = 16
+    ("ViT-L/14@336px", "fp16", 8, False),  # P = 14: patch rows padded to 16 pixels, Kp = 704
+    ("ViT-L/14@336px", "fp16", 8, True),   # 16-bit pixels, P = 14: the padded cast ran anyway
+])
+def test_patch_im2col_is_bit_identical(gpu, name, dtype, B, pix16):
+    """The explicit patch GEMM (tuning patch_im2col: blocked im2col written by the cast pass, then
+    the pipelined 160x128 tile on blocked A and W) uses the implicit GEMM's k order and k-tile
+    sequence, so the features equal the implicit GEMM's bit for bit."""
+    cfg = C.get_config(name)
+    sd = synthetic_state_dict(cfg, 0)
+    px = _pixels(B, cfg.image_size, seed=61).to(gpu)
+    if pix16:
+        px = px.to(torch.float16 if dtype == "fp16" else torch.bfloat16)
+    outs = []
+    for im2col in (1, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(patch_im2col=im2col))
+        try:
+            eng.load_state_dict(sd)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (name, dtype, B)
