@@ -119,6 +119,13 @@ __device__ __forceinline__ i32x4_t buf_rsrc(const void* base, unsigned bytes) {
 __device__ __forceinline__ void blds16(i32x4_t rsrc, unsigned voff, int soff, void* lds_wave_base) {
     raw_buffer_load_lds(rsrc, (LDS_AS void*)lds_wave_base, 16, (int)voff, soff, 0, 0);
 }
+// 16-byte store through a buffer resource (buffer_store_dwordx4 ... offen): per-lane byte offset,
+// range-checked (an offset past the resource's byte count writes nothing). aux 2 = non-temporal.
+// A kernel whose counted vmcnt waits include its epilogue stores issues them this way, so the
+// number of store instructions does not depend on how many rows are valid (a branch around an
+// all-masked store would drop it from the count).
+__device__ void raw_buffer_store_v4i32(i32x4_t data, i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v4i32");
 
 // ---- MX-fp8: OCP e4m3 elements, one E8M0 (power-of-two) scale per 32 consecutive K ----
 // Block rule (shared by every producer and by the tests' host reference): e = the smallest

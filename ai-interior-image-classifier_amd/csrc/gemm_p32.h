@@ -211,7 +211,11 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             : "v"(ba)
             : "memory");
     };
-    unsigned char* const Cb = (unsigned char*)a.C;
+    // C through a range-checked resource: rows >= M (row-major) fall outside it and are dropped,
+    // so every epilogue issues exactly 2 FM stores (the counted waits W_HI below rely on it);
+    // blocked C keeps the padding rows of its last 16-row block inside the resource (the consumer
+    // reads them only into unstored rows). The launcher checks the C bytes fit 32 bits.
+    const i32x4_t rs_out = buf_rsrc(a.C, (unsigned)((size_t)(a.blk_c ? ((a.M + 15) & ~15) : a.M) * a.ldc * 2));
     auto epilogue = [&](int pm0, int pn0) {
         // lane-derived addresses recomputed here from an opaque copy of the lane id: hipcc
         // otherwise hoists the per-row offsets of all 16 stores out of the tile loop and spills
@@ -237,9 +241,9 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             }
             u32x4 w0 = {pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]), pack2<T>(v[6], v[7])};
             u32x4 w1 = {pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]), pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])};
-            size_t off, off2;
+            unsigned off, off2;
             if (a.blk_c) {  // blocked C: each quarter-wave already writes 256 contiguous bytes
-                off = blk16_off(m, n, a.ldc);
+                off = (unsigned)blk16_off(m, n, a.ldc);
                 off2 = off + 256;
             } else {
                 // row-major C: lane group g holds features [16g, 16g + 16) of the wave's 64-column
@@ -255,17 +259,13 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
                     w1[d] = r[1];
                 }
                 const int g = le >> 4;
-                off = ((size_t)m * a.ldc + (n - 16 * g)) * 2 + 32 * (g & 1) + 16 * (g >> 1);
+                off = ((unsigned)m * (unsigned)a.ldc + (unsigned)(n - 16 * g)) * 2u + 32u * (g & 1) + 16u * (g >> 1);
                 off2 = off + 64;
             }
-            if (m < a.M && (HK::ABL != 3 || a.ldc < 0)) {
-                if constexpr (NT) {
-                    __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
-                    __builtin_nontemporal_store(w1, (u32x4*)(Cb + off2));
-                } else {
-                    *(u32x4*)(Cb + off) = w0;
-                    *(u32x4*)(Cb + off2) = w1;
-                }
+            if (m >= a.M && !a.blk_c) off = off2 = 0xFFFFFFF0u;  // outside the resource: dropped
+            if constexpr (HK::ABL != 3) {
+                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w0), rs_out, (int)off, 0, NT ? 2 : 0);
+                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w1), rs_out, (int)off2, 0, NT ? 2 : 0);
             }
             __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
         }

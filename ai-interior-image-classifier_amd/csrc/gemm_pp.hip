@@ -327,6 +327,7 @@ template <typename T, bool BLKW, bool NT, int BM = 256>
 static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a, bool balanced = false) {
     if (a.K % 128 || a.K < 256) return -1;  // whole groups of four 32-deep k-steps, >= 2 groups
     if (a.N > (BM == 256 ? 8192 : 4096)) return -1;  // the bias vector's LDS room (gemm_p32_kernel)
+    if ((size_t)(a.M + 15) * a.ldc * 2 >= 0xFFFFFFF0u) return -1;  // C offsets are 32-bit (gemm_p32.h rs_out)
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + BM - 1) / BM) * (a.N / 256);
     const int per = (ntiles + ncu - 1) / ncu;
