@@ -642,7 +642,7 @@ static int gemm8(hipStream_t s, clipvit_handle* h, int epi, const unsigned char*
         if (rc == 0) h->log_launch(role, v, g.M, LOG_MX8 | (g.blk_a ? LOG_BLK_A : 0) | (g.blk_c ? LOG_BLK_C : 0));
         return rc;
     };
-    if (v8 == 3 && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // ping-pong: 1-D maps
+    if ((v8 == 3 || v8 == 4) && xcd_split_n(N / 256, a.xcd_n)) a.xcd_n = 0;  // persistent MX tiles: 1-D maps
     // Whole-round row split of the MX c_fc (as gemm()'s for the 16-bit one): when the 256x256
     // tiles fill R whole rounds plus at most half a round (B/32 lane of 256 images: 600 tiles =
     // 2 rounds + 88), rows [0, M1) run on the persistent ping-pong and rows [M1, M) on the
@@ -792,9 +792,9 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
         else ln(ly.ln2g, ly.ln2b, qm);
         if (prof) prof->mark(s, F_LN);
         const bool p16 = r16 && !last;
-        // blocked u8: both MLP GEMMs on the persistent MX tile, whose epilogues are STORE / GELU_Q8
+        // blocked u8: both MLP GEMMs on the persistent MX tiles (c_fc 3 or 4), whose epilogues are STORE / GELU_Q8
         // (the fp32 residual c_proj runs on the other MX tiles: row-major u8)
-        const bool ublk = h->u_blk && p16 && h->var8[R_FC] == 3 && h->var8[R_PROJ] == 3;
+        const bool ublk = h->u_blk && p16 && (h->var8[R_FC] == 3 || h->var8[R_FC] == 4) && h->var8[R_PROJ] == 3;
         rc = qm ? gemm8(s, h, EPI_GELU_Q8, q8, ly.wfc, ly.bfc, u8, M, 4 * D, D, 4 * D, R_FC, ublk)
                : gemm(s, h, EPI_GELU, w->h, ly.wfc, ly.bfc, w->u, M, 4 * D, D, 4 * D, R_FC, Fold(), w, ly.wfc_b);
         if (rc) return rc;

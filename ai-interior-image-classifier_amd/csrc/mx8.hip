@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <type_traits>
 #include "common.h"
+#include "gemm_p32mx.h"
 
 namespace clipvit {
 
@@ -783,6 +784,28 @@ static int launch_mx8_pp(hipStream_t s, int epi, const GemmArgs& a, bool persist
     return -1;
 }
 
+// Variant 4: gemm_p32mx.h (the 32x32x64 scaled MFMA on the 4-stage 64-deep-k-step ring), balanced
+// persistent grid (the fewest workgroups with the same tiles per workgroup). Row-major A.
+template <typename TO>
+static int launch_mx8_p32(hipStream_t s, int epi, const GemmArgs& a) {
+    if (a.N % 256 || a.N > 4096 || a.K % 256 || a.K < 512 || a.blk_a || xcd_split_n(a.N / 256, a.xcd_n)) return -1;
+    if ((size_t)(a.M + 15) * a.ldc * 4 >= 0xFFFFFFC0u) return -1;  // 32-bit epilogue offsets
+    const int ncu = a.ncu > 0 ? a.ncu : 256;
+    const int ntiles = ((a.M + 255) / 256) * (a.N / 256);
+    const int per = (ntiles + ncu - 1) / ncu;
+    const int grid = (ntiles + per - 1) / per;
+    if (epi == EPI_STORE && !a.blk_c) { gemm_mx8_p32_kernel<TO, EPI_STORE, false><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_F32 && !a.blk_c) { gemm_mx8_p32_kernel<TO, EPI_F32, false><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_F32GELU && !a.blk_c) { gemm_mx8_p32_kernel<TO, EPI_F32GELU, false><<<grid, 512, 0, s>>>(a, ntiles); return 0; }
+    if (epi == EPI_GELU_Q8) {
+        if (a.blk_c != (a.sc_rows != 0)) return -1;  // blocked u8 goes with its blocked scales
+        if (a.blk_c) gemm_mx8_p32_kernel<TO, EPI_GELU_Q8, true><<<grid, 512, 0, s>>>(a, ntiles);
+        else gemm_mx8_p32_kernel<TO, EPI_GELU_Q8, false><<<grid, 512, 0, s>>>(a, ntiles);
+        return 0;
+    }
+    return -1;
+}
+
 // variant: 0 auto, 1 128x256 (2x4 waves), 2 128x128 (2x2 waves), 3 ping-pong 256x256
 // persistent, 5 160x128 (2x2 waves; two per CU,
 // 480 tiles = one round at M = 12,800, N = 768)
@@ -793,6 +816,7 @@ static int launch_mx8_t(hipStream_t s, int epi, const GemmArgs& a, int variant) 
         case 1: return launch_mx8_tile<TO, 128, 256, 2, 4>(s, epi, a);
         case 2: return launch_mx8_tile<TO, 128, 128, 2, 2>(s, epi, a);
         case 3: return launch_mx8_pp<TO>(s, epi, a, true);
+        case 4: return launch_mx8_p32<TO>(s, epi, a);
         case 5: return launch_mx8_tile<TO, 160, 128, 2, 2>(s, epi, a);
     }
     return -1;
@@ -803,7 +827,7 @@ int launch_gemm_mx8(hipStream_t s, int out16, int epi, const GemmArgs& a, int va
     // blocked u8: read by the persistent ping-pong only; written by it or (c_fc tail launch of
     // the whole-round row split) by the 128 x 128 / 160 x 128 tiles' QuickGELU + quantize epilogue
     if (a.blk_a && variant != 3) return -1;
-    if (a.blk_c && variant != 3 && variant != 2 && variant != 5) return -1;
+    if (a.blk_c && variant != 3 && variant != 4 && variant != 2 && variant != 5) return -1;
     if (a.blk_c && (epi != EPI_GELU_Q8 || a.ldc % 128)) return -1;
     if ((epi == EPI_GELU_Q8 || epi == EPI_Q8) && (!a.sC || a.ldc % 32)) return -1;
     if (out16 == 2) return launch_mx8_t<F16>(s, epi, a, variant);

@@ -110,7 +110,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * LDS transpose (2, default)); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
  * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
  * trace_gemm (0/1: clipvit_gemm_log);
- * large_variants "q,f,o,p"; mx8_variants "q,o,f,p"; mx8_skip / mx8_skip_mlp "i,j,.." (bf16
+ * large_variants "q,f,o,p"; mx8_variants "q,o,f,p" (3 = ping-pong 256x256, 4 = the 32x32x64 scaled-MFMA
+ * form of the 32-deep-k-step tile, QKV / c_fc only); mx8_skip / mx8_skip_mlp "i,j,.." (bf16
  * blocks; mx8_skip sets both masks). An unknown key or bad value fails with CLIPVIT_E_INVALID
  * and leaves the handle unchanged. The product path never calls it. */
 int clipvit_set_tuning(clipvit_handle* h, const char* spec);

@@ -166,6 +166,47 @@ def test_gemm_mx8_epilogues(gpu):
     assert torch.equal(c5, c0.to(torch.bfloat16))
 
 
+@pytest.mark.parametrize("M,N,K", [(257, 512, 512), (1000, 2304, 768), (333, 768, 3072),
+                                   (12800, 2304, 768), (12800, 3072, 768), (25600, 3072, 768)])
+def test_gemm_mx8_p32_tile(gpu, M, N, K):
+    """MX variant 4 (gemm_p32mx.h: 32x32x64 scaled MFMA on the 4-stage 64-deep-k-step ring). Its
+    fp32 sums group 64 products per instruction (variants 1-3: 128), so it is checked against
+    the fp64 product of the same quantized operands (1e-4 of max|C|, the bar of the other
+    tiles), and its own outputs against each other bit for bit: the bf16 store equals the
+    rounding of its fp32 output, the MX-fp8 QuickGELU output the quantization of its fp32
+    QuickGELU output (launch_quant_mx8), over repeated launches (race screen)."""
+    A8, sA, W, bias, Ad, Wd = _quantized_operands(gpu, M, N, K, M + N + K + 2)
+    c0 = E.gemm_mx8_test(A8, sA, W, bias, epi=0, variant=4)
+    ref = Ad @ Wd.T + bias.cpu().numpy()[None, :]
+    err = np.abs(c0.cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err < 1e-4, err
+    c1 = E.gemm_mx8_test(A8, sA, W, bias, epi=1, variant=4)
+    gelu = torch.from_numpy(ref).float()
+    gelu = gelu * torch.sigmoid(1.702 * gelu)
+    assert ((c1.cpu() - gelu).abs().max() / gelu.abs().max()).item() < 1e-4
+    c5 = E.gemm_mx8_test(A8, sA, W, bias, epi=5, variant=4)
+    assert torch.equal(c5, c0.to(torch.bfloat16))
+    q_ref, s_ref = E.quant_mx8_test(c1)
+    for rep in range(3):
+        q, s = E.gemm_mx8_test(A8, sA, W, bias, epi=4, variant=4)
+        assert torch.equal(s, s_ref) and torch.equal(q, q_ref), rep
+        assert torch.equal(E.gemm_mx8_test(A8, sA, W, bias, epi=5, variant=4), c5), rep
+        assert torch.equal(E.gemm_mx8_test(A8, sA, W, bias, epi=0, variant=4), c0), rep
+
+
+def test_gemm_mx8_p32_exact_integers(gpu):
+    """Small integers are exact in e4m3 under any scale: variant 4's C equals the integer product
+    (ragged M: the last 256-row tile is mostly rows past M, dropped by the store range check)."""
+    M, N, K = 300, 512, 1024
+    g = torch.Generator().manual_seed(12)
+    A = torch.randint(-3, 4, (M, K), generator=g).float()
+    W = torch.randint(-3, 4, (N, K), generator=g).float()
+    W[:, ::5] = 0
+    A8, sA = E.quant_mx8_test(A.to(gpu))
+    Cg = E.gemm_mx8_test(A8, sA, W.to(gpu), None, epi=0, variant=4).cpu()
+    assert torch.equal(Cg, A @ W.t())
+
+
 # ---------------------------------------------------------------- end to end (config 5)
 def _engine(cfg, dtype, sd, adapters, T, segs, gpu, B, tuning=None):
     eng = VisionEngine(cfg, gpu, dtype, max_batch=B, tuning=tuning)
