@@ -235,6 +235,205 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// attention_p_kernel: the one-key-block attention (N <= 64, the ViT-B/32 shape) as a persistent
+// loop. attention_v2<SINGLE> runs one (image, head) unit per workgroup: its K/V DMA, Q loads,
+// 16 MFMAs and stores form one dependent chain of ~3 memory latencies per 25 KB moved, and at
+// 8 workgroups per CU the chip is latency-bound (r06 profile: 4.3 TB/s of fabric traffic, wait
+// share 0.36). Here a workgroup walks units u = blockIdx.x + i * gridDim.x with a 2-stage K/V
+// ring: unit i + 1's K/V DMA and Q loads are issued before unit i is computed, so the loads of
+// one unit overlap the arithmetic and stores of the previous one. Per unit the arithmetic is
+// attention_v2<SINGLE>'s, instruction for instruction (the same bits).
+template <typename T, bool Q8 = false>
+__global__ __launch_bounds__(256, 2) void attention_p_kernel(const u16* __restrict__ qkv, u16* __restrict__ out, int B,
+                                                            int N, int H, unsigned char* __restrict__ q8 = nullptr,
+                                                            unsigned char* __restrict__ q8s = nullptr) {
+    typedef typename T::vec8 vec8;
+    constexpr int QW = 4, STAGE = 2 * 64 * 128;  // K [64][128 B] | V [64][128 B]
+    __shared__ __attribute__((aligned(16))) unsigned char smem[2 * STAGE];
+    const int D = H * 64, ld = 3 * D;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & 15, g = lane >> 4;
+    const int q = wave * 16 + j, qc = min(q, N - 1);
+    const int units = B * H, G = gridDim.x;
+    constexpr int RW = 64 / QW, LPB = 2 * (RW / 8);  // K/V rows per wave; LDS-DMA pieces per wave and unit
+    const unsigned range = (unsigned)((size_t)(N - 1) * ld * 2 + (size_t)D * 2 + 128);
+
+    auto issue = [&](int u, int st) {  // unit u's K/V -> stage st (rows >= N read as zeros)
+        const int b = u / H, h = u - b * H;
+        const unsigned char* src = (const unsigned char*)(qkv + (size_t)b * N * ld + D + h * 64);
+        const i32x4_t rs = buf_rsrc(src, range);
+        unsigned char* dst = smem + st * STAGE;
+#pragma unroll
+        for (int r = 0; r < RW / 8; ++r) {
+            const int row = wave * RW + r * 8 + (lane >> 3);
+            const int c = (lane & 7) ^ (row & 7);
+            const unsigned off = (unsigned)(row * ld * 2 + c * 16);
+            blds16(rs, off, 0, dst + (wave * RW + r * 8) * 128);
+            blds16(rs, off + (unsigned)D * 2, 0, dst + 8192 + (wave * RW + r * 8) * 128);
+        }
+    };
+    // Q rows by inline-asm loads: invisible to hipcc's waitcnt pass, which would otherwise wait
+    // for the NEXT unit's loads (vmcnt(0)) before the current unit's first MFMA; they are covered
+    // by the counted wait below instead, and the two register sets alternate (no copies)
+    auto load_q = [&](int u, vec8 (&qd)[2]) {
+        const int b = u / H, h = u - b * H;
+        const u16* qrow = qkv + ((size_t)b * N + qc) * ld + h * 64 + 8 * g;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qd[0]) : "v"(qrow) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(qd[1]) : "v"(qrow) : "memory");
+    };
+
+    int u = blockIdx.x;
+    if (u >= units) return;
+    vec8 qa[2], qb[2];
+    issue(u, 0);
+    load_q(u, qa);
+    const float scale = 0.125f;  // 1/sqrt(64)
+    // one unit: K/V in stage st, Q in qf; prefetches the next unit's K/V / Q into stage st ^ 1 /
+    // qn. Returns false after the workgroup's last unit.
+    auto unit = [&](int st, vec8 (&qf)[2], vec8 (&qn)[2]) -> bool {
+        const int un = u + G;
+        const bool more = un < units;
+        // the other stage was last read by the previous unit: every wave is past it (barrier at
+        // the end of that unit)
+        if (more) {
+            issue(un, st ^ 1);
+            load_q(un, qn);
+            vm_wait<LPB + 2>();  // this unit's pieces and Q landed (the next unit's are the youngest LPB + 2)
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // ... every wave's
+        const unsigned char* Ks = smem + st * STAGE;
+        const unsigned char* Vs = Ks + 8192;
+
+        f32x4 o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        float m_run = -INFINITY, l_run = 0.f;
+        f32x4 s[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int row = kt * 16 + j;
+#pragma unroll
+            for (int ds = 0; ds < 2; ++ds) {
+                const int c = ((ds << 2) | g) ^ (row & 7);
+                const vec8 kf = *(const vec8*)(Ks + row * 128 + (c << 4));
+                s[kt] = T::mfma16(kf, qf[ds], s[kt]);
+            }
+        }
+        float mloc = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = kt * 16 + 4 * g + r;
+                const float v = key < N ? s[kt][r] * scale : -INFINITY;
+                s[kt][r] = v;
+                mloc = fmaxf(mloc, v);
+            }
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 16, 64));
+        mloc = fmaxf(mloc, __shfl_xor(mloc, 32, 64));
+        const float m_new = fmaxf(m_run, mloc);
+        const float alpha = __expf(m_run - m_new);
+        m_run = m_new;
+        float lsum = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float p = __expf(s[kt][r] - m_new);
+                s[kt][r] = p;
+                lsum += p;
+            }
+        l_run = l_run * alpha + lsum;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] *= alpha;
+        const int tq = (lane & 15) >> 2, tp = lane & 3;
+        const unsigned vbase = (unsigned)(size_t)(LDS_AS const unsigned char*)Vs;
+#pragma unroll
+        for (int stp = 0; stp < 2; ++stp) {
+            u32x2 vr[4][2];
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const int k = 32 * stp + 16 * hf + 4 * g + tq;
+                    const int cl = 2 * dt + (tp >> 1);
+                    const unsigned addr = vbase + k * 128 + ((cl ^ (k & 7)) << 4) + 8 * (tp & 1);
+                    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(vr[dt][hf]) : "v"(addr) : "memory");
+                }
+            vec8 pf;
+            {
+                unsigned w[4] = {pack2<T>(s[2 * stp][0], s[2 * stp][1]), pack2<T>(s[2 * stp][2], s[2 * stp][3]),
+                                 pack2<T>(s[2 * stp + 1][0], s[2 * stp + 1][1]),
+                                 pack2<T>(s[2 * stp + 1][2], s[2 * stp + 1][3])};
+                pf = __builtin_bit_cast(vec8, *(uint4*)w);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const uint4 vv = make_uint4(vr[dt][0].x, vr[dt][0].y, vr[dt][1].x, vr[dt][1].y);
+                o[dt] = T::mfma16(__builtin_bit_cast(vec8, vv), pf, o[dt]);
+            }
+        }
+        l_run += __shfl_xor(l_run, 16, 64);
+        l_run += __shfl_xor(l_run, 32, 64);
+        const int b = u / H, h = u - b * H;
+        const size_t base = (size_t)b * N;
+        if constexpr (Q8) {
+            const float inv = 1.0f / l_run;
+            float v[4][4], am[2] = {0.f, 0.f};
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+                for (int r = 0; r < 4; r += 2) {
+                    const unsigned w = pack2<T>(o[dt][r] * inv, o[dt][r + 1] * inv);
+                    v[dt][r] = T::to_f32((u16)(w & 0xffff));
+                    v[dt][r + 1] = T::to_f32((u16)(w >> 16));
+                    am[dt >> 1] = fmaxf(am[dt >> 1], fmaxf(fabsf(v[dt][r]), fabsf(v[dt][r + 1])));
+                }
+#pragma unroll
+            for (int bk = 0; bk < 2; ++bk) {
+                am[bk] = fmaxf(am[bk], __shfl_xor(am[bk], 16, 64));
+                am[bk] = fmaxf(am[bk], __shfl_xor(am[bk], 32, 64));
+            }
+            if (q < N) {
+                const int e0 = mx_exp(am[0]), e1 = mx_exp(am[1]);
+                const float i0 = mx_inv(e0), i1 = mx_inv(e1);
+                unsigned char* qrow8 = q8 + (base + q) * D + h * 64;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const float iv = dt < 2 ? i0 : i1;
+                    *(unsigned*)(qrow8 + dt * 16 + 4 * g) =
+                        pk4_e4m3(v[dt][0] * iv, v[dt][1] * iv, v[dt][2] * iv, v[dt][3] * iv);
+                }
+                if (g < 2) q8s[(base + q) * (D / 32) + h * 2 + g] = (unsigned char)((g == 0 ? e0 : e1) + 127);
+            }
+        } else if (q < N) {
+            const float inv = 1.0f / l_run;
+            u16* orow = out + (base + q) * D + h * 64;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                uint2 w;
+                w.x = pack2<T>(o[dt][0] * inv, o[dt][1] * inv);
+                w.y = pack2<T>(o[dt][2] * inv, o[dt][3] * inv);
+                *(uint2*)(orow + dt * 16 + 4 * g) = w;
+            }
+        }
+        if (!more) return false;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's reads of stage st done
+        __builtin_amdgcn_s_barrier();        // ... every wave's: the unit after next may refill it
+        u = un;
+        return true;
+    };
+    while (unit(0, qa, qb) && unit(1, qb, qa)) {
+    }
+}
+
 // Online-softmax update of one 16-query fragment over a 64-key block (attention_v3, N > 128).
 // s holds the raw Q.K scores of the lane's 16 keys (key = kb*64 + 16 kt + 4 g + r). The softmax
 // runs in the log2 domain:
@@ -436,22 +635,38 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 8 : 2) void attention_v3_kernel(c
 // attention with the output quantized to MX-fp8 (q8 [B N, D] e4m3 + q8s [B N, D / 32] scales) in
 // the kernel, for the shapes that run on the one-key-block attention_v2 (N <= 64: ViT-B/32);
 // returns -1 otherwise (the caller then runs launch_attention + launch_quant_mx8, the same bytes)
+// persist > 0: attention_p_kernel on persist workgroups per CU (ncu CUs), else one workgroup per
+// (image, head)
+static int attn_grid(int units, int persist, int ncu) {
+    const int g = persist * (ncu > 0 ? ncu : 256);
+    return g < units ? g : units;
+}
 int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,
-                        int B, int N, int H) {
+                        int B, int N, int H, int persist, int ncu) {
     if (N > 64) return -1;
-    dim3 grid(1, H, B), block(256);
     const u16* in = (const u16*)qkv;
+    if (persist > 0) {
+        const int G = attn_grid(B * H, persist, ncu);
+        if (dtype == 2) attention_p_kernel<F16, true><<<G, 256, 0, s>>>(in, nullptr, B, N, H, q8, q8s);
+        else attention_p_kernel<BF16, true><<<G, 256, 0, s>>>(in, nullptr, B, N, H, q8, q8s);
+        return 0;
+    }
+    dim3 grid(1, H, B), block(256);
     if (dtype == 2) attention_v2_kernel<F16, 4, true, false, true><<<grid, block, 0, s>>>(in, nullptr, N, H, q8, q8s);
     else attention_v2_kernel<BF16, 4, true, false, true><<<grid, block, 0, s>>>(in, nullptr, N, H, q8, q8s);
     return 0;
 }
 
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
-                      bool causal) {
+                      bool causal, int persist, int ncu) {
     dim3 grid((N + 63) / 64, H, B), block(256);
     const u16* in = (const u16*)qkv;
     u16* o = (u16*)out;
-    if (causal) {  // text tower: key blocks past the workgroup's last query are skipped
+    if (!causal && N <= 64 && persist > 0) {  // one key block: the persistent loop
+        const int G = attn_grid(B * H, persist, ncu);
+        if (dtype == 2) attention_p_kernel<F16><<<G, 256, 0, s>>>(in, o, B, N, H);
+        else attention_p_kernel<BF16><<<G, 256, 0, s>>>(in, o, B, N, H);
+    } else if (causal) {  // text tower: key blocks past the workgroup's last query are skipped
         if (dtype == 2) attention_v2_kernel<F16, 4, false, true><<<grid, block, 0, s>>>(in, o, N, H);
         else attention_v2_kernel<BF16, 4, false, true><<<grid, block, 0, s>>>(in, o, N, H);
     } else if (N > 128) {  // long sequences: 4 waves x 32 queries

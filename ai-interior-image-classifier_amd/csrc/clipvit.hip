@@ -286,6 +286,10 @@ struct clipvit_handle {
     // layout) + the pipelined 160x128 tile on blocked A and W, instead of the implicit GEMM over
     // the cast pixels (tuning patch_im2col; only where a cast pass runs anyway)
     int patch_im2col = 1;
+    // one-key-block attention (N <= 64: ViT-B/32) as a persistent loop on attn_persist workgroups
+    // per CU, each prefetching its next (image, head) unit (attention_p_kernel); 0 = one
+    // workgroup per unit (attention_v2)
+    int attn_persist = 0;
     int use_hblk() const { return use_x24() && !lnfold ? h_blk : 0; }
     // test hook (tuning trace_gemm=1): every role GEMM launch of gemm() / gemm8() appends
     // {role, tile variant, M, flags} here (clipvit_gemm_log), so a test can assert which kernel
@@ -771,8 +775,8 @@ static int forward_mx8(clipvit_handle* h, hipStream_t s, const void* pix, int in
                : gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b);
         if (rc) return rc;
         if (prof) prof->mark(s, F_QKV);
-        if (!q || !h->attn_q8 || launch_attention_q8(s, h->dt, w->qkv, q8, q8s, B, N, h->cfg.heads) != 0) {
-            launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        if (!q || !h->attn_q8 || launch_attention_q8(s, h->dt, w->qkv, q8, q8s, B, N, h->cfg.heads, h->attn_persist, h->ncu) != 0) {
+            launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
             if (q) launch_quant_mx8(s, h->dt, w->h, q8, q8s, M, D);
         }
         if (prof) prof->mark(s, F_ATTN);
@@ -891,7 +895,7 @@ static int forward_fold(clipvit_handle* h, hipStream_t s, const void* pix, int i
         fq.s = ly.s_qkv; fq.st_in = w->st; fq.np = np;
         if ((rc = gemm(s, h, EPI_LNF, w->h, ly.wqkv, ly.bf_qkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, fq))) return rc;
         if (prof) prof->mark(s, F_QKV);
-        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
         if (prof) prof->mark(s, F_ATTN);
         if (i + 1 == nl && h->cls_prune) {
             if ((rc = cls_tail_fold(h, s, B, w, f_out, prof, X24))) return rc;
@@ -948,7 +952,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
         if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
-        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads);
+        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
         if (prof) prof->mark(s, F_ATTN);
         if (last && h->cls_prune) {
             if ((rc = cls_tail(h, s, B, w, f_out, prof, X24, X24 != nullptr))) return rc;
@@ -1209,6 +1213,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 2;
     else if (k == "patch_im2col") ok = parse_int(v, h->patch_im2col) && (h->patch_im2col == 0 || h->patch_im2col == 1);
+    else if (k == "attn_persist") ok = parse_int(v, h->attn_persist) && h->attn_persist >= 0 && h->attn_persist <= 4;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 62, 72, 74)
         int m[2] = {h->split_main, h->split_tail};
@@ -1270,13 +1275,13 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
-        int h_blk, patch_im2col, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int h_blk, patch_im2col, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1292,7 +1297,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;
@@ -1864,7 +1869,9 @@ int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* o
                            int H, int causal) {
     g_err.clear();
     if (!qkv_dev || !out_dev || B <= 0 || N <= 0 || H <= 0) FAIL(CLIPVIT_E_INVALID, "bad argument");
-    launch_attention((hipStream_t)stream, dtype, qkv_dev, out_dev, B, N, H, causal != 0);
+    // causal: bit 0 = causal mask; causal >> 4 = workgroups per CU of the persistent one-key-block
+    // kernel (tuning attn_persist; 0 = one workgroup per unit)
+    launch_attention((hipStream_t)stream, dtype, qkv_dev, out_dev, B, N, H, (causal & 1) != 0, causal >> 4, current_ncu());
     HIPCHK(hipGetLastError());
     return 0;
 }

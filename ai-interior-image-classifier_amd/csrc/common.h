@@ -426,10 +426,12 @@ void launch_embed_stats(hipStream_t s, int dtype, float* x, void* x16, float2* s
                         void* x24 = nullptr);
 
 
+// persist > 0 (N <= 64, non-causal): the persistent attention_p_kernel on persist workgroups per CU
+// (ncu CUs; 0 = 256), else one workgroup per (image, head, 64-query block)
 int launch_attention_q8(hipStream_t s, int dtype, const void* qkv, unsigned char* q8, unsigned char* q8s,
-                        int B, int N, int H);
+                        int B, int N, int H, int persist = 0, int ncu = 0);
 void launch_attention(hipStream_t s, int dtype, const void* qkv, void* out, int B, int N, int H,
-                      bool causal = false);
+                      bool causal = false, int persist = 0, int ncu = 0);
 
 void launch_embed_ln(hipStream_t s, int dtype, float* x, void* h, const float* cls,
                      const float* pos, const float* g_pre, const float* b_pre, const float* g1,

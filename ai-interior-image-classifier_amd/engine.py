@@ -281,10 +281,12 @@ def residual_x24_test(x: torch.Tensor) -> torch.Tensor:
     return back
 
 
-def attention_test(qkv: torch.Tensor, B: int, N: int, H: int, causal: bool = False) -> torch.Tensor:
+def attention_test(qkv: torch.Tensor, B: int, N: int, H: int, causal: bool = False, persist: int = 0) -> torch.Tensor:
+    """clipvit_attention_test; persist > 0 (N <= 64): the persistent one-key-block kernel on that
+    many workgroups per CU (tuning attn_persist)."""
     L = _lib.lib()
     out = torch.empty((B * N, H * 64), dtype=qkv.dtype, device=qkv.device)
     with torch.cuda.device(qkv.device):
         s = ctypes.c_void_p(torch.cuda.current_stream(qkv.device).cuda_stream)
-        _lib.check(L.clipvit_attention_test(s, _DT[qkv.dtype], _vp(qkv), _vp(out), B, N, H, int(causal)))
+        _lib.check(L.clipvit_attention_test(s, _DT[qkv.dtype], _vp(qkv), _vp(out), B, N, H, int(causal) | (persist << 4)))
     return out

@@ -109,6 +109,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * h_blocked (0/1/2: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
  * LDS transpose (2, default)); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
  * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
+ * attn_persist (0..4: N <= 64 attention as a persistent loop on that many workgroups per CU);
  * trace_gemm (0/1: clipvit_gemm_log);
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p" (3 = ping-pong 256x256, 4 = the 32x32x64 scaled-MFMA
  * form of the 32-deep-k-step tile, QKV / c_fc only); mx8_skip / mx8_skip_mlp "i,j,.." (bf16
@@ -284,7 +285,9 @@ int clipvit_gemm_mx8_test(void* stream, const unsigned char* A8_dev, const unsig
 int clipvit_residual_x24_test(void* stream, const float* x_dev, void* planes_dev, float* back_dev, size_t n);
 
 /* softmax(Q K^T / sqrt(64)) V for a packed qkv [B*N, 3*H*64] buffer of `dtype`;
- * out [B*N, H*64] of `dtype`. causal != 0: key j masked for query i < j (the text tower). */
+ * out [B*N, H*64] of `dtype`. causal bit 0: key j masked for query i < j (the text tower);
+ * causal >> 4 = k > 0 with N <= 64: the persistent one-key-block kernel on k workgroups per CU
+ * (tuning attn_persist). */
 int clipvit_attention_test(void* stream, int dtype, const void* qkv_dev, void* out_dev, int B,
                            int N, int H, int causal);
 

@@ -220,6 +220,25 @@ def test_attention_tail_rows_never_read(gpu, B, N, H, causal):
     assert err < 3e-3, err
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,N,H,persist", [(3, 50, 12, 1), (256, 50, 12, 2), (256, 50, 12, 1), (7, 64, 12, 2),
+                                           (5, 1, 12, 1), (300, 33, 12, 3), (1, 50, 2, 4)])
+def test_attention_persistent_bit_identical(gpu, dtype, B, N, H, persist):
+    """The persistent one-key-block attention (tuning attn_persist: each workgroup walks several
+    (image, head) units, prefetching the next unit's K/V / Q while computing the current one) runs
+    attention_v2's per-unit arithmetic: its output equals attention_v2's bit for bit, for fewer
+    units than workgroups, several units per workgroup and ragged N; repeated launches agree, and
+    NaN rows past the last image are never read."""
+    g = torch.Generator(device=gpu).manual_seed(B * N + H + persist)
+    big = torch.full((B * N + 128, 3 * H * 64), float("nan"), device=gpu, dtype=dtype)
+    big[:B * N] = (torch.randn(B * N, 3 * H * 64, device=gpu, generator=g) * 1.5).to(dtype)
+    qkv = big[:B * N]
+    ref = E.attention_test(qkv, B, N, H)
+    for rep in range(3):
+        out = E.attention_test(qkv, B, N, H, persist=persist)
+        assert torch.equal(out, ref), (rep, (out.float() - ref.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
                                    (36928 // 4, 4096, 1024)])
 def test_ping_pong_race_screen(gpu, M, N, K):

@@ -589,3 +589,24 @@ def test_patch_im2col_is_bit_identical(gpu, name, dtype, B, pix16):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B)
+
+
+@pytest.mark.parametrize("dtype,persist", [("fp16", 2), ("bf16", 1), ("mxfp8", 2)])
+def test_attention_persistent_engine_bit_identical(gpu, dtype, persist):
+    """ViT-B/32 (N = 50) with the persistent one-key-block attention (tuning attn_persist; for
+    MX-fp8 its quantizing epilogue) gives the same features as the one-workgroup-per-unit kernel,
+    bit for bit."""
+    cfg = C.get_config("ViT-B/32")
+    sd = synthetic_state_dict(cfg, 0)
+    px = _pixels(64, cfg.image_size, seed=67).to(gpu)
+    outs = []
+    for p in (persist, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=64, tuning=dict(attn_persist=p))
+        try:
+            eng.load_state_dict(sd)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (dtype, persist)
