@@ -281,7 +281,7 @@ struct clipvit_handle {
     // B/32 bs 256 83.45-83.49k -> 83.76-84.14k img/s with 2 (c_fc 0.81 -> 0.784 ms per forward,
     // LayerNorm +0.018), 83.08-83.48k with 1 (profiles/r06/hblk_inmodel_ab.txt). QKV's h stays
     // row-major: its 240x256 tile measured the same either way (profiles/r06/hblk_v1_inmodel_ab.txt)
-    int h_blk = 2;
+    int h_blk = 3;
     // patch embedding as blocked im2col (the pixel cast writes the GEMM's A in the 16-row blocked
     // layout) + the pipelined 160x128 tile on blocked A and W, instead of the implicit GEMM over
     // the cast pixels (tuning patch_im2col; only where a cast pass runs anyway)
@@ -1211,7 +1211,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
     else if (k == "trace_gemm") ok = flag(h->trace);
-    else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 2;
+    else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 3;
     else if (k == "patch_im2col") ok = parse_int(v, h->patch_im2col) && (h->patch_im2col == 0 || h->patch_im2col == 1);
     else if (k == "attn_persist") ok = parse_int(v, h->attn_persist) && h->attn_persist >= 0 && h->attn_persist <= 4;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;

@@ -208,6 +208,10 @@ __device__ __forceinline__ void store_row16_blk(u16* h, int row, const float4 (&
 __device__ __forceinline__ int hblk_lds_off(int b, int c, int m) {
     return (b << 11) + (c << 8) + ((m ^ (c | ((b & 1) << 3))) << 4);
 }
+// The same for an 8-row half group (HBLK 3): 128-B runs per (block b, chunk c), row slot XOR c
+__device__ __forceinline__ int hblk8_lds_off(int b, int c, int m) {
+    return (b << 10) + (c << 7) + ((m ^ c) << 4);
+}
 
 // MX-fp8 row store: lanes 8j..8j+7 hold the 32 consecutive columns of block j (per i), so the
 // block amax is an xor-shuffle over 8 lanes; each lane writes its 4 e4m3 bytes, lane 8j the
@@ -391,7 +395,9 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // (a wave-instruction writes 32 scattered 16-B chunks). 2: RPW = 4, so a workgroup owns one 16-row
 // group: its rows' outputs go to LDS in the blocked order and leave as one contiguous run (32 D
 // bytes); rows past `rows` in the last group (padding rows of the buffer) carry the last row's
-// values.
+// values. 3: RPW = 2, a workgroup owns half a 16-row group (8 rows): twice the workgroups (1,600
+// at B/32 bs 256 against 800, whose 3.1 per CU left a quarter of the last round idle), and the
+// rows leave as 128-B runs (8 rows x one 16-B chunk).
 template <typename T, int V, bool STORE_X = true, bool TWO = false, int RPW = 1, bool Q8 = false, bool X16 = false,
           bool X24 = false, int HBLK = 0>
 __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ xv, const u16* __restrict__ y,
@@ -399,8 +405,9 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
                                                             const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
-    constexpr bool BLKH = HBLK == 2;
-    static_assert(!BLKH || (RPW == 4 && !Q8), "blocked h: 16 rows per workgroup, 16-bit output");
+    constexpr bool BLKH = HBLK >= 2;
+    constexpr int GROUP = 4 * RPW;  // rows per workgroup
+    static_assert(!BLKH || (RPW == (HBLK == 2 ? 4 : 2) && !Q8), "blocked h: 16 / 8 rows per workgroup, 16-bit output");
     static_assert(HBLK != 1 || !Q8, "blocked h: 16-bit output");
     // RPW rows per wave, every row's loads issued before any row's arithmetic (more bytes in
     // flight per wave; rows / RPW waves fit one residency round of the CUs at bs 256)
@@ -427,7 +434,7 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
             if constexpr (TWO) w2[r][i] = *(const uint2*)(y2 + (size_t)row * D + (lane + 64 * i) * 4);
         }
     }
-    constexpr int HLDS = BLKH ? 32 * D : 16;
+    constexpr int HLDS = BLKH ? GROUP * 2 * D : 16;
     __shared__ __attribute__((aligned(16))) unsigned char hs[HLDS];
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
@@ -458,22 +465,31 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
         ln_row<V>(v[r], gm, bt, lane, (float)D);
         if constexpr (Q8) store_row_q8<V>((unsigned char*)h + (size_t)row * D, sq + (size_t)row * (D / 32), v[r], lane);
         else if constexpr (BLKH) {
-            const int m = (threadIdx.x >> 6) * RPW + r;  // row slot inside the 16-row group
+            const int m = (threadIdx.x >> 6) * RPW + r;  // row slot inside the workgroup's rows
 #pragma unroll
             for (int i = 0; i < V; ++i) {
                 const int c = (lane + 64 * i) * 4;
-                const int off = hblk_lds_off(c >> 6, (c & 63) >> 3, m) + ((c & 7) << 1);
+                const int off = (HBLK == 2 ? hblk_lds_off(c >> 6, (c & 63) >> 3, m) : hblk8_lds_off(c >> 6, (c & 63) >> 3, m)) +
+                                ((c & 7) << 1);
                 *(uint2*)(hs + off) = make_uint2(pack2<T>(v[r][i].x, v[r][i].y), pack2<T>(v[r][i].z, v[r][i].w));
             }
         } else if constexpr (HBLK == 1) {
             store_row16_blk<T, V>((u16*)h, row, v[r], lane);
         } else store_row16<T, V>((u16*)h + (size_t)row * D, v[r], lane);
     }
-    if constexpr (BLKH) {  // the group's 32 D bytes, contiguous in the blocked layout
+    if constexpr (HBLK == 2) {  // the group's 32 D bytes, contiguous in the blocked layout
         __syncthreads();
         unsigned char* dst = (unsigned char*)h + (size_t)blockIdx.x * 32 * D;
         for (int o = threadIdx.x * 16; o < 32 * D; o += 256 * 16)
             *(uint4*)(dst + o) = *(const uint4*)(hs + hblk_lds_off(o >> 11, (o >> 8) & 7, (o >> 4) & 15));
+    } else if constexpr (HBLK == 3) {  // 16 D bytes as 128-B runs: rows m0..m0+7 of each (block, chunk)
+        __syncthreads();
+        const int m0 = blockIdx.x * 8;
+        unsigned char* dst = (unsigned char*)h + (size_t)(m0 >> 4) * 32 * D + (m0 & 15) * 16;
+        for (int o = threadIdx.x * 16; o < 16 * D; o += 256 * 16) {
+            const int run = o >> 7, b = run >> 3, c = run & 7, m = (o >> 4) & 7;
+            *(uint4*)(dst + b * 2048 + c * 256 + m * 16) = *(const uint4*)(hs + hblk8_lds_off(b, c, m));
+        }
     }
 }
 
@@ -631,6 +647,10 @@ static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2,
         dim3 grid((rows + 15) / 16), block(256);
         if (y2) add_layernorm_kernel<T, V, true, true, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
         else add_layernorm_kernel<T, V, false, false, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+    } else if constexpr (HBLK == 3) {  // two workgroups per 16-row group (4 waves x 2 rows)
+        dim3 grid((rows + 15) / 16 * 2), block(256);
+        if (y2) add_layernorm_kernel<T, V, true, true, 2, false, X16, X24, 3><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 2, false, X16, X24, 3><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
     } else {
         dim3 grid((rows + 3) / 4), block(256);
         if (y2) add_layernorm_kernel<T, V, true, true, 1, false, X16, X24, HBLK><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
@@ -689,6 +709,11 @@ void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const voi
     if (x24 && hblk == 2) {
         if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        return;
+    }
+    if (x24 && hblk == 3) {
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 3>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 3>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         return;
     }
     if (x24) {

@@ -106,8 +106,8 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * qkv_variant / fc_variant (100 * XCD map + tile of the QKV / c_fc role only); fc_balanced (0/1:
  * c_fc with >= 2 whole rounds of 256x256 tiles plus a remainder as one balanced launch, default 1,
  * or as the round split of split_variants); fc_balanced_variant (75 / 77: its tile);
- * h_blocked (0/1/2: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
- * LDS transpose (2, default)); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
+ * h_blocked (0..3: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
+ * LDS transpose of 16-row (2) or 8-row (3, default) groups per workgroup); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
  * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
  * attn_persist (0..4: N <= 64 attention as a persistent loop on that many workgroups per CU);
  * trace_gemm (0/1: clipvit_gemm_log);

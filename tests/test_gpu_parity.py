@@ -525,7 +525,7 @@ def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun, fc):
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[1], outs[2]), (name, dtype, B, tun)
 
 
-@pytest.mark.parametrize("hmode", [1, 2])
+@pytest.mark.parametrize("hmode", [1, 2, 3])
 @pytest.mark.parametrize("name,dtype,B,tun", [
     ("ViT-B/32", "fp16", 256, {}),                 # c_fc v75
     ("ViT-B/32", "fp16", 128, {}),                 # c_fc round split v62 + v81
