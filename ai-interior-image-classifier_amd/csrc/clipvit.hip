@@ -286,6 +286,9 @@ struct clipvit_handle {
     // layout) + the pipelined 160x128 tile on blocked A and W, instead of the implicit GEMM over
     // the cast pixels (tuning patch_im2col; only where a cast pass runs anyway)
     int patch_im2col = 1;
+    // rows per wave of the add + LayerNorm after c_proj (ln_1 of the next block, 24-bit stream):
+    // 1 (3,200 workgroups at B/32 bs 256) or 2 (1,600)
+    int ln1_rows = 1;
     // one-key-block attention (N <= 64: ViT-B/32) as a persistent loop on attn_persist workgroups
     // per CU, each prefetching its next (image, head) unit (attention_p_kernel); 0 = one
     // workgroup per unit (attention_v2)
@@ -980,7 +983,8 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                 return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr);
+            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr,
+                                                     X24 && h->ln1_rows == 2 ? 4 : 0);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -1213,6 +1217,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 3;
     else if (k == "patch_im2col") ok = parse_int(v, h->patch_im2col) && (h->patch_im2col == 0 || h->patch_im2col == 1);
+    else if (k == "ln1_rows") ok = parse_int(v, h->ln1_rows) && (h->ln1_rows == 1 || h->ln1_rows == 2);
     else if (k == "attn_persist") ok = parse_int(v, h->attn_persist) && h->attn_persist >= 0 && h->attn_persist <= 4;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
     else if (k == "split_variants") {  // "main[,tail]": main a 256x256 tile (8, 62, 72, 74)
@@ -1275,13 +1280,13 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
-        int h_blk, patch_im2col, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int h_blk, patch_im2col, ln1_rows, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->ln1_rows, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1297,7 +1302,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->ln1_rows = before.ln1_rows; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;

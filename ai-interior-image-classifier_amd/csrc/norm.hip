@@ -405,7 +405,7 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
                                                             void* __restrict__ h, unsigned char* __restrict__ sq,
                                                             const float* __restrict__ gm,
                                                             const float* __restrict__ bt, int rows) {
-    constexpr bool BLKH = HBLK >= 2;
+    constexpr bool BLKH = HBLK == 2 || HBLK == 3;
     constexpr int GROUP = 4 * RPW;  // rows per workgroup
     static_assert(!BLKH || (RPW == (HBLK == 2 ? 4 : 2) && !Q8), "blocked h: 16 / 8 rows per workgroup, 16-bit output");
     static_assert(HBLK != 1 || !Q8, "blocked h: 16-bit output");
@@ -647,6 +647,10 @@ static void add_ln_deferred(hipStream_t s, void* x, const u16* y, const u16* y2,
         dim3 grid((rows + 15) / 16), block(256);
         if (y2) add_layernorm_kernel<T, V, true, true, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
         else add_layernorm_kernel<T, V, false, false, 4, false, X16, X24, 2><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
+    } else if constexpr (HBLK == 4) {  // row-major h, 2 rows per wave (half the workgroups of RPW 1)
+        dim3 grid((rows + 7) / 8), block(256);
+        if (y2) add_layernorm_kernel<T, V, true, true, 2, false, X16, X24, 0><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
+        else add_layernorm_kernel<T, V, false, false, 2, false, X16, X24, 0><<<grid, block, 0, s>>>(x, y, nullptr, h, nullptr, g, b, rows);
     } else if constexpr (HBLK == 3) {  // two workgroups per 16-row group (4 waves x 2 rows)
         dim3 grid((rows + 15) / 16 * 2), block(256);
         if (y2) add_layernorm_kernel<T, V, true, true, 2, false, X16, X24, 3><<<grid, block, 0, s>>>(x, y, y2, h, nullptr, g, b, rows);
@@ -709,6 +713,11 @@ void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const voi
     if (x24 && hblk == 2) {
         if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 2>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        return;
+    }
+    if (x24 && hblk == 4) {  // (not a layout: row-major h from 2 rows per wave)
+        if (dtype == 2) DISPATCH_V(D, (add_ln_deferred<F16, V, false, true, 4>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
+        else DISPATCH_V(D, (add_ln_deferred<BF16, V, false, true, 4>(s, x16, yy, yy2, (u16*)h, g, b, rows)))
         return;
     }
     if (x24 && hblk == 3) {

@@ -109,7 +109,7 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * h_blocked (0..3: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
  * LDS transpose of 16-row (2) or 8-row (3, default) groups per workgroup); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
  * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
- * attn_persist (0..4: N <= 64 attention as a persistent loop on that many workgroups per CU);
+ * ln1_rows (1/2: rows per wave of the add + LayerNorm after c_proj, default 1); attn_persist (0..4: N <= 64 attention as a persistent loop on that many workgroups per CU);
  * trace_gemm (0/1: clipvit_gemm_log);
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p" (3 = ping-pong 256x256, 4 = the 32x32x64 scaled-MFMA
  * form of the 32-deep-k-step tile, QKV / c_fc only); mx8_skip / mx8_skip_mlp "i,j,.." (bf16

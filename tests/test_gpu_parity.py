@@ -610,3 +610,23 @@ def test_attention_persistent_engine_bit_identical(gpu, dtype, persist):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (dtype, persist)
+
+
+@pytest.mark.parametrize("name,dtype,B", [("ViT-B/32", "fp16", 256), ("ViT-B/32", "bf16", 67), ("ViT-B/16", "fp16", 33)])
+def test_ln1_rows_is_bit_identical(gpu, name, dtype, B):
+    """The add + LayerNorm after c_proj with two rows per wave (tuning ln1_rows=2; ragged row
+    counts leave the last wave one row) does each row's arithmetic as with one: same features."""
+    cfg = C.get_config(name)
+    sd = synthetic_state_dict(cfg, 0)
+    px = _pixels(B, cfg.image_size, seed=71).to(gpu)
+    outs = []
+    for r in (2, 1):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(ln1_rows=r))
+        try:
+            eng.load_state_dict(sd)
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (name, dtype, B)
