@@ -156,8 +156,10 @@ struct clipvit_handle {
     // of 256x256): in-model QKV 0.673 -> 0.662 ms per forward. c_fc on 22 in one launch since
     // the 4-wave tiles keep their accumulators in VGPRs (gemm_pipe_kernel launch bounds): c_fc
     // 0.795 ms per forward as with the round split (8 + 81), c_proj after it 0.675 -> 0.658 ms,
-    // B/32 bs 256 85.6k -> 86.3k img/s (2 same-box alternations)
-    int var[5] = {98, 82, 22, 82, 22};
+    // B/32 bs 256 85.6k -> 86.3k img/s (2 same-box alternations). r06: QKV on the 32-deep-k-step
+    // tile (72) with its A in the blocked layout (qkv_blk): QKV family 0.626 -> 0.615 ms per
+    // forward on 72 alone, 0.580 -> 0.560 with the blocked A (profiles/r06/qkv_ab.txt)
+    int var[5] = {72, 82, 22, 82, 22};
     bool var_forced = false;  // tuning gemm_variants given: no shape-based override
     // tile of the QKV / c_fc roles at large M (>= 4 rounds of 256x256 tiles), 100 * XCD map +
     // tile; 0 = the 2-phase 256x256 tile (8). Default: the persistent ping-pong tile with the
@@ -176,7 +178,7 @@ struct clipvit_handle {
     // 0/1 = 1-D bijective remap. out_proj / c_proj use the 1-D remap: same speed as the 4x2 grid
     // (c_proj 69.9 vs 70.0 us, out 24.0 vs 24.1) with each A panel read by one XCD instead of
     // two: PMC bytes / algorithmic 1.61 -> 1.13 (c_proj) and 1.33 -> 1.02 (out_proj)
-    int xcd[5] = {2, 0, 2, 0, 1};
+    int xcd[5] = {0, 0, 2, 0, 1};
     int split_min = SPLIT_NEVER;  // batch size from which the two lane streams are used (clipvit_create)
     // MX-fp8 mode (compute_dtype CLIPVIT_MXFP8): the four Linears of every block run as
     // MX-fp8 GEMMs (packed weight = N*Kp e4m3 bytes followed by N*Kp/32 E8M0 scales);
@@ -289,6 +291,9 @@ struct clipvit_handle {
     // rows per wave of the add + LayerNorm after c_proj (ln_1 of the next block, 24-bit stream):
     // 1 (3,200 workgroups at B/32 bs 256) or 2 (1,600)
     int ln1_rows = 1;
+    // QKV's A in the 16-row blocked layout too (blocks 1..L-1: ln_1 after c_proj writes it as
+    // ln_2 does for c_fc, h_blocked's 8-row form; block 0's comes row-major from embed_ln)
+    int qkv_blk = 1;
     // one-key-block attention (N <= 64: ViT-B/32) as a persistent loop on attn_persist workgroups
     // per CU, each prefetching its next (image, head) unit (attention_p_kernel); 0 = one
     // workgroup per unit (attention_v2)
@@ -566,9 +571,16 @@ static int gemm(hipStream_t s, clipvit_handle* h, int epi, const void* A, const 
             variant = lv % 100;
         }
     }
-    // a tuned variant that does not tile this shape falls back to the shape-based choice
+    // a tuned variant that does not tile this shape (or, for the persistent tiles >= 60, lacks
+    // the epilogue: the LayerNorm-fold ones) falls back to a pipelined tile, then the shape-based
+    // choice
     wsel(a, variant);
     int rc = launch(a, variant);
+    if (rc != 0 && variant >= 60) {
+        const int fv = N % 256 == 0 ? 98 : 22;
+        wsel(a, fv);
+        rc = launch(a, fv);
+    }
     wsel(a, 0);
     if (rc != 0 && launch(a, 0) != 0) {
         g_err = "gemm: unsupported shape M=" + std::to_string(M) + " N=" + std::to_string(N) +
@@ -939,6 +951,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     // X24: the residual stream in 24-bit planes (w->x then only holds the patch GEMM's rows)
     void* X24 = h->use_x24() ? w->x16 : nullptr;
     const int hb = h->use_hblk();
+    const bool hq = hb != 0 && h->qkv_blk;  // blocked h for QKV (blocks >= 1)
     launch_embed_ln(s, h->dt, w->x, w->h, h->cls, h->pos, h->lnpre_g, h->lnpre_b, l0.ln1g, l0.ln1b,
                     B, N, D, X24, X24 != nullptr);
     if (prof) prof->mark(s, F_EMBED);
@@ -952,7 +965,8 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
     for (int i = 0; i < nl; ++i) {
         const LayerW& ly = h->layers[i];
         const bool last = i + 1 == nl;
-        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b)))
+        if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wqkv, ly.bqkv, w->qkv, M, 3 * D, D, 3 * D, R_QKV, Fold(), w, ly.wqkv_b,
+                       hq && i > 0)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
         launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
@@ -984,7 +998,7 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
             if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr,
-                                                     X24 && h->ln1_rows == 2 ? 4 : 0);
+                                                     hq ? 3 : X24 && h->ln1_rows == 2 ? 4 : 0);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -1217,6 +1231,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "trace_gemm") ok = flag(h->trace);
     else if (k == "h_blocked") ok = parse_int(v, h->h_blk) && h->h_blk >= 0 && h->h_blk <= 3;
     else if (k == "patch_im2col") ok = parse_int(v, h->patch_im2col) && (h->patch_im2col == 0 || h->patch_im2col == 1);
+    else if (k == "qkv_blk") ok = parse_int(v, h->qkv_blk) && (h->qkv_blk == 0 || h->qkv_blk == 1);
     else if (k == "ln1_rows") ok = parse_int(v, h->ln1_rows) && (h->ln1_rows == 1 || h->ln1_rows == 2);
     else if (k == "attn_persist") ok = parse_int(v, h->attn_persist) && h->attn_persist >= 0 && h->attn_persist <= 4;
     else if (k == "w_blocked") ok = parse_int(v, h->w_blk) && h->w_blk >= 0 && h->w_blk <= 2;
@@ -1280,13 +1295,13 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
         bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
-        int h_blk, patch_im2col, ln1_rows, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
+        int h_blk, patch_im2col, ln1_rows, qkv_blk, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->ln1_rows, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->ln1_rows, g->qkv_blk, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1302,7 +1317,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->ln1_rows = before.ln1_rows; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->ln1_rows = before.ln1_rows; h->qkv_blk = before.qkv_blk; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;

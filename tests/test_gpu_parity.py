@@ -484,7 +484,7 @@ def test_blocked_u_is_bit_identical(gpu, name, dtype, B, tun, fc):
 
 
 @pytest.mark.parametrize("name,dtype,B,tun,fc", [
-    ("ViT-B/32", "fp16", 256, {}, [75]),                      # QKV v98, c_fc v75, out / c_proj v82: all read the copy (2)
+    ("ViT-B/32", "fp16", 256, {}, [75]),                      # QKV v72, c_fc v75, out / c_proj v82: all read the copy (2)
     ("ViT-B/32", "fp16", 256, {"split_variants": "72,81", "fc_balanced": 0}, [72, 81]),  # c_fc main 72 + tail 81
     ("ViT-B/32", "fp16", 256, {"fc_balanced": 0}, [62, 81]),  # the round split (v62 reads the copy, the tail follows it)
     ("ViT-B/32", "fp16", 128, {}, [62, 81]),                  # bs 128: the round split by default
@@ -535,10 +535,10 @@ def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun, fc):
     ("ViT-L/14@336px", "fp16", 32, {}),            # D = 1024
 ])
 def test_blocked_h_is_bit_identical(gpu, name, dtype, B, tun, hmode):
-    """ln_2's output h in the 16-row blocked layout (tuning h_blocked: 1 = direct stores, 2 = an
-    LDS transpose in the LN kernel; c_fc stages 1 KB runs) moves bytes only: the features equal
-    the row-major run's bit for bit, and the launch log shows c_fc (and only c_fc) reading a
-    blocked A."""
+    """ln_2's output h in the 16-row blocked layout (tuning h_blocked: 1 = direct stores, 2 / 3 = an
+    LDS transpose of 16 / 8 rows in the LN kernel; c_fc stages 1 KB runs) moves bytes only: the
+    features equal the row-major run's bit for bit, and the launch log shows c_fc reading a blocked
+    A (and QKV from block 1, qkv_blk) exactly when h_blocked is on."""
     cfg = C.get_config(name)
     sd = synthetic_state_dict(cfg, 0)
     ad = synthetic_adapters(cfg, rank=8)
@@ -554,7 +554,8 @@ def test_blocked_h_is_bit_identical(gpu, name, dtype, B, tun, hmode):
             torch.cuda.synchronize()
             log = eng.gemm_log()
             assert {bool(f & 4) for r, _, _, f in log if r == 2} == {bool(hb)}, (hb, log)  # c_fc
-            assert {bool(f & 4) for r, _, _, f in log if r == 0} == {False}, (hb, log)    # QKV
+            qkv = [bool(f & 4) for r, _, _, f in log if r == 0]  # QKV: blocked from block 1 (qkv_blk)
+            assert any(qkv) == bool(hb) and not all(qkv), (hb, log)
         finally:
             eng.close()
     assert torch.isfinite(outs[0]).all()
@@ -630,3 +631,34 @@ def test_ln1_rows_is_bit_identical(gpu, name, dtype, B):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B)
+
+
+@pytest.mark.parametrize("name,dtype,B,tun", [
+    ("ViT-B/32", "fp16", 256, {}),                      # QKV v98 (pipelined 240x256) on blocked A
+    ("ViT-B/32", "fp16", 256, {"qkv_variant": 72}),     # QKV on the 32-deep-k-step tile
+    ("ViT-B/32", "bf16", 67, {"qkv_variant": 72}),      # ragged M
+    ("ViT-B/16", "fp16", 256, {}),                      # two lanes, large-M tile
+    ("ViT-L/14@336px", "fp16", 32, {}),                 # D = 1024
+])
+def test_blocked_qkv_h_is_bit_identical(gpu, name, dtype, B, tun):
+    """ln_1 (the add + LayerNorm after c_proj) writing QKV's A in the 16-row blocked layout
+    (tuning qkv_blk; block 0's h stays row-major from embed_ln) moves bytes only: the features
+    equal the row-major run's bit for bit, and the launch log shows blocked-A QKV launches only
+    with the option on."""
+    cfg = C.get_config(name)
+    sd = synthetic_state_dict(cfg, 0)
+    px = _pixels(B, cfg.image_size, seed=73).to(gpu)
+    outs = []
+    for qb in (1, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, qkv_blk=qb, trace_gemm=1))
+        try:
+            eng.load_state_dict(sd)
+            eng.gemm_log()
+            outs.append(eng.encode_image(px).clone())
+            torch.cuda.synchronize()
+            flags = [bool(f & 4) for r, _, _, f in eng.gemm_log() if r == 0]
+            assert any(flags) == bool(qb) and not all(flags), (qb, flags)
+        finally:
+            eng.close()
+    assert torch.isfinite(outs[0]).all()
+    assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
