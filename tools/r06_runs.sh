@@ -116,9 +116,10 @@ run_tiles() {
 # the round's profile (tools/profile_round.sh: kernel trace + FETCH / WRITE / MFMA / L2 passes,
 # then the default bench with its PMC traffic) and the other configurations' bench lines
 run_closing() {
-  out=gpurun_out/r06_closing
+  tag=${1:-r06}
+  out=gpurun_out/${tag}_closing
   mkdir -p $out
-  timeout -k 10 1100 bash tools/profile_round.sh gpurun_out/prof_r06 r06 > $out/profile.log 2>&1 \
+  timeout -k 10 1100 bash tools/profile_round.sh gpurun_out/prof_$tag $tag > $out/profile.log 2>&1 \
     || { echo "profile round failed"; tail -20 $out/profile.log; exit 1; }
   tail -2 $out/profile.log
   for c in "cfg4|--model ViT-L/14@336px --batch 128 --lora-rank 16 --steps 5 --warmup 2" \
