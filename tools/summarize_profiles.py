@@ -46,6 +46,8 @@ def roles_for_trace(rows):
             out.append("patch_gemm"); seg = None; continue
         if "im2col" in n:
             out.append("im2col"); continue
+        if out and out[-1] == "im2col" and gemm_like(n):  # the explicit patch GEMM on the im2col matrix
+            out.append("patch_gemm"); seg = None; continue
         if "embed_ln" in n or "embed_stats" in n:
             out.append("embed"); seg = [] ; continue
         if "gather_cls" in n:  # last block on class-token rows (cls_tail)
