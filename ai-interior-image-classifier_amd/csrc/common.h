@@ -116,8 +116,10 @@ __device__ __forceinline__ i32x4_t buf_rsrc(const void* base, unsigned bytes) {
     r.w = 0x00020000;  // gfx9 raw buffer: DATA_FORMAT 32, no swizzle
     return r;
 }
+// AUX: the cache-policy bits of the load (gfx950: 1 sc0, 2 nt, 16 sc1)
+template <int AUX = 0>
 __device__ __forceinline__ void blds16(i32x4_t rsrc, unsigned voff, int soff, void* lds_wave_base) {
-    raw_buffer_load_lds(rsrc, (LDS_AS void*)lds_wave_base, 16, (int)voff, soff, 0, 0);
+    raw_buffer_load_lds(rsrc, (LDS_AS void*)lds_wave_base, 16, (int)voff, soff, 0, AUX);
 }
 // 16-byte store through a buffer resource (buffer_store_dwordx4 ... offen): per-lane byte offset,
 // range-checked (an offset past the resource's byte count writes nothing). aux 2 = non-temporal.
@@ -126,6 +128,35 @@ __device__ __forceinline__ void blds16(i32x4_t rsrc, unsigned voff, int soff, vo
 // all-masked store would drop it from the count).
 __device__ void raw_buffer_store_v4i32(i32x4_t data, i32x4_t rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.store.v4i32");
+
+// Cache policy of the GEMM epilogue stores (gfx950 bits: 1 sc0, 2 nt, 16 sc1). sc0 sc1 (17)
+// writes the line through and drops it from the XCD's L2 (MI355X_MICROARCH.md, store flavours),
+// so a tile's output does not evict the operand panels the XCD's other tiles are still reading.
+// r06 same-box A/B on the 32-deep-k-step tile (QKV, c_fc): QKV 0.542 -> 0.523 ms, c_fc 0.676 ->
+// 0.655 ms per forward, B/32 +1.2-1.5 % against plain stores; nt loads of A: -5 %
+// (profiles/r06/store_policy_ab.txt).
+#ifndef GEMM_ST_AUX
+#define GEMM_ST_AUX 17
+#endif
+// 16-byte store at byte offset off of the buffer rs (wave-uniform base), with cache policy AUX
+template <int AUX>
+__device__ __forceinline__ void st16_pol(const i32x4_t& rs, size_t off, const uint4& v) {
+    raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, v), rs, (int)(unsigned)off, 0, AUX);
+}
+// 16-byte store at byte offset off (< 4 GB) of the wave-uniform base C: a plain global store for
+// AUX 0, else a buffer store with those policy bits
+template <int AUX>
+__device__ __forceinline__ void cstore16(void* C, size_t off, const uint4& v) {
+    if constexpr (AUX == 0) *(uint4*)((unsigned char*)C + off) = v;
+    else st16_pol<AUX>(buf_rsrc(C, 0xFFFFFFFFu), off, v);
+}
+// store policy of the ping-pong (gemm_pp.hip) and MX-fp8 (mx8.hip, gemm_p32mx.h) tiles
+#ifndef PP_AUX_ST
+#define PP_AUX_ST 0
+#endif
+#ifndef MX_AUX_ST
+#define MX_AUX_ST 0
+#endif
 
 // ---- MX-fp8: OCP e4m3 elements, one E8M0 (power-of-two) scale per 32 consecutive K ----
 // Block rule (shared by every producer and by the tests' host reference): e = the smallest

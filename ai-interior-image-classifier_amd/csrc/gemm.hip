@@ -326,6 +326,22 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
 }
 
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
+// C stores of the pipelined tiles' epilogues (16-bit C, the patch rows): cache policy PIPE_AUX_ST
+// (0 = plain global stores; otherwise buffer stores over C with those policy bits; default sc0
+// sc1, common.h GEMM_ST_AUX). r06 same box, B/32 bs 256: out_proj 0.245 -> 0.225 ms, c_proj
+// 0.665 -> 0.658 ms per forward, +1.1 % against plain stores (profiles/r06/store_policy_ab.txt)
+#ifndef PIPE_AUX_ST
+#define PIPE_AUX_ST GEMM_ST_AUX
+#endif
+__device__ __forceinline__ i32x4_t c_rsrc(const GemmArgs& a) {
+    const size_t bytes = (size_t)((a.M + 15) & ~15) * a.ldc * 2;  // (blocked C: rows padded to 16)
+    return buf_rsrc(a.C, (unsigned)(bytes < 0xFFFFFFFFu ? bytes : 0xFFFFFFFFu));
+}
+__device__ __forceinline__ void c_store(unsigned char* Cb, const i32x4_t& rs, size_t off, const uint4& v) {
+    if constexpr (PIPE_AUX_ST == 0) *(uint4*)(Cb + off) = v;
+    else st16_pol<PIPE_AUX_ST>(rs, off, v);
+}
+
 template <typename T, int BM, int BN, int WM, int WN, int NS, int EPI, int SM = 0, int PIMPL = 0>
 __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_kernel(GemmArgs a) {
     typedef typename T::vec8 vec8;
@@ -655,13 +671,14 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_s_barrier();
         unsigned char* Cb = (unsigned char*)a.C;
+        const i32x4_t rs_c = c_rsrc(a);
         if (a.blk_c) {  // blocked C: a quarter-wave stores one chunk of 16 rows (256 B contiguous)
 #pragma unroll 4
             for (int i = tid; i < BM * CPR; i += NT) {
                 const int r = ((i >> 4) / CPR) * 16 + (i & 15), c = (i >> 4) % CPR;
                 const int m = m0 + r;
                 const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
-                if (m < a.M) *(uint4*)(Cb + blk16_off(m, n0 + 8 * c, a.ldc)) = val;
+                if (m < a.M) c_store(Cb, rs_c, blk16_off(m, n0 + 8 * c, a.ldc), val);
             }
             return;
         }
@@ -670,7 +687,7 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
             const int r = i / CPR, c = i % CPR;
             const int m = m0 + r;
             const uint4 val = *(const uint4*)(smem + r * ROWB + ((c ^ (r & 7)) << 4));
-            if (m < a.M) *(uint4*)(Cb + ((size_t)m * a.ldc + n0) * 2 + c * 16) = val;
+            if (m < a.M) c_store(Cb, rs_c, ((size_t)m * a.ldc + n0) * 2 + c * 16, val);
         }
         return;
     }
@@ -720,10 +737,11 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                 // blocked C: n % 16 == 0, so n + 8 is the next chunk of the same 64-block (+256 B)
                 const size_t off = a.blk_c ? blk16_off(m, n, a.ldc) : ((size_t)m * a.ldc + n) * 2;
                 const size_t off2 = a.blk_c ? off + 256 : off + 16;
-                *(uint4*)(Cb + off) = (make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
-                                       pack2<T>(v[6], v[7])));
-                *(uint4*)(Cb + off2) = (make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
-                                            pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
+                const i32x4_t rs_c = c_rsrc(a);
+                c_store(Cb, rs_c, off, make_uint4(pack2<T>(v[0], v[1]), pack2<T>(v[2], v[3]), pack2<T>(v[4], v[5]),
+                                                  pack2<T>(v[6], v[7])));
+                c_store(Cb, rs_c, off2, make_uint4(pack2<T>(v[8], v[9]), pack2<T>(v[10], v[11]),
+                                                   pack2<T>(v[12], v[13]), pack2<T>(v[14], v[15])));
             } else if constexpr (EPI == EPI_RESID) {
                 const float4* src = (const float4*)((float*)a.C + (size_t)m * a.ldc + n);
                 const size_t off = ((size_t)m * a.ldc + n) * 4;
@@ -739,8 +757,11 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                     row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
                 const size_t off = (row * a.ldc + n) * 4;
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    *(float4*)(Cb + off + 16 * i) = (make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]));
+                for (int i = 0; i < 4; ++i) {
+                    const float4 o = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+                    if constexpr (EPI == EPI_PATCH) cstore16<PIPE_AUX_ST>(Cb, off + 16 * i, __builtin_bit_cast(uint4, o));
+                    else *(float4*)(Cb + off + 16 * i) = o;
+                }
             }
         }
     }

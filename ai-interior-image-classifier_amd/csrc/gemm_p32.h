@@ -44,6 +44,22 @@
 
 #include "common.h"
 
+// Cache-policy bits of the p32 tile's operand loads (A pieces, W pieces) and epilogue stores
+// (gfx950: 1 sc0, 2 nt, 16 sc1; an NT instantiation stores with nt; default stores: GEMM_ST_AUX,
+// common.h). Build-time A/B knobs (tools/build_alt.py).
+#ifndef P32_AUX_A
+#define P32_AUX_A 0
+#endif
+#ifndef P32_AUX_W
+#define P32_AUX_W 0
+#endif
+#ifndef P32_AUX_ST
+#define P32_AUX_ST GEMM_ST_AUX
+#endif
+#ifndef P32_AUX_NT
+#define P32_AUX_NT 2
+#endif
+
 namespace clipvit {
 
 // Hook policy of gemm_p32_kernel. The library's: barriers only, no ablation. The probe's policy
@@ -123,7 +139,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         unsigned char* dst = smem + st * STAGE + opbase + NP * wc * 1024;
         const int so = koff(kk);
 #pragma unroll
-        for (int i = 0; i < NP; ++i) blds16(r, voff[i], so, dst + i * 1024);
+        for (int i = 0; i < NP; ++i) blds16<GRP == 0 ? P32_AUX_A : P32_AUX_W>(r, voff[i], so, dst + i * 1024);
     };
 
     int m0, n0, mn = 0, nn = 0;
@@ -264,8 +280,8 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             }
             if (m >= a.M && !a.blk_c) off = off2 = 0xFFFFFFF0u;  // outside the resource: dropped
             if constexpr (HK::ABL != 3) {
-                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w0), rs_out, (int)off, 0, NT ? 2 : 0);
-                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w1), rs_out, (int)off2, 0, NT ? 2 : 0);
+                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w0), rs_out, (int)off, 0, NT ? P32_AUX_NT : P32_AUX_ST);
+                raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w1), rs_out, (int)off2, 0, NT ? P32_AUX_NT : P32_AUX_ST);
             }
             __builtin_amdgcn_sched_barrier(0);  // one row block at a time (register pressure)
         }

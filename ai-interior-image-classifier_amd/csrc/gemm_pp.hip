@@ -280,8 +280,8 @@ __global__ __launch_bounds__(512, 1) void gemm_ppp_kernel(GemmArgs a, int ntiles
                     __builtin_nontemporal_store(w0, (u32x4*)(Cb + off));
                     __builtin_nontemporal_store(w1, (u32x4*)(Cb + off2));
                 } else {
-                    *(u32x4*)(Cb + off) = w0;
-                    *(u32x4*)(Cb + off2) = w1;
+                    cstore16<PP_AUX_ST>(Cb, off, __builtin_bit_cast(uint4, w0));
+                    cstore16<PP_AUX_ST>(Cb, off2, __builtin_bit_cast(uint4, w1));
                 }
             }
         }

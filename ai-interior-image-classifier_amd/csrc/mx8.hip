@@ -365,11 +365,11 @@ __global__ __launch_bounds__(64 * WM* WN, 2) void gemm_mx8_kernel(GemmArgs a) {
                 const int e = mx_exp(am);
                 const float inv = mx_inv(e);
                 // blocked C (blk_c, blk8_off): the quarter-wave's 16 rows x 16 B are 256 contiguous bytes
-                *(uint4*)((unsigned char*)a.C + (a.blk_c ? blk8_off(m, n, a.ldc) : (size_t)m * a.ldc + n)) =
+                cstore16<MX_AUX_ST>(a.C, a.blk_c ? blk8_off(m, n, a.ldc) : (size_t)m * a.ldc + n,
                     make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
                                pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
-                               pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
+                               pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv)));
                 if ((g & 1) == 0)
                     a.sC[a.sc_rows ? ((size_t)(n >> 7) * a.sc_rows + m) * 4 + ((n >> 5) & 3)
                                    : (size_t)m * (a.ldc / 32) + (n >> 5)] = (unsigned char)(e + 127);
@@ -738,19 +738,19 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                         co = (unsigned)m * (unsigned)a.ldc + (unsigned)n;
                         so = (unsigned)m * (unsigned)(a.ldc / 32) + (unsigned)(n >> 5);
                     }
-                    *(uint4*)((unsigned char*)a.C + co) =
+                    cstore16<MX_AUX_ST>(a.C, co,
                         make_uint4(pk4_e4m3(v[0] * inv, v[1] * inv, v[2] * inv, v[3] * inv),
                                    pk4_e4m3(v[4] * inv, v[5] * inv, v[6] * inv, v[7] * inv),
                                    pk4_e4m3(v[8] * inv, v[9] * inv, v[10] * inv, v[11] * inv),
-                                   pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv));
+                                   pk4_e4m3(v[12] * inv, v[13] * inv, v[14] * inv, v[15] * inv)));
                     if ((eg & 1) == 0) a.sC[so] = (unsigned char)(e + 127);
                 }
             } else if (m < a.M) {  // EPI_STORE
-                uint4* dst = (uint4*)((u16*)a.C + (size_t)m * a.ldc + n);
-                dst[0] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                                    pack2<TO>(v[6], v[7]));
-                dst[1] = make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]), pack2<TO>(v[12], v[13]),
-                                    pack2<TO>(v[14], v[15]));
+                const size_t off = ((size_t)m * a.ldc + n) * 2;
+                cstore16<MX_AUX_ST>(a.C, off, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]),
+                                                         pack2<TO>(v[4], v[5]), pack2<TO>(v[6], v[7])));
+                cstore16<MX_AUX_ST>(a.C, off + 16, make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]),
+                                                              pack2<TO>(v[12], v[13]), pack2<TO>(v[14], v[15])));
             }
         }
         if (!has_next) break;
