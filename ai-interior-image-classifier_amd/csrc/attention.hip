@@ -46,6 +46,11 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // `out`: each value rounded to T first, then quantized by the launch_quant_mx8 rule, so the bytes
 // equal attention + quant_mx8 exactly. MX block b of a head = features 32 b .. 32 b + 31 = the
 // lane's dt 2b, 2b+1 values across the 4 lanes of its query (g = 0..3).
+// store policy of the attention output (common.h gst; 0 = plain stores)
+#ifndef ATT_AUX_ST
+#define ATT_AUX_ST 0
+#endif
+
 template <typename T, int QW = 4, bool SINGLE = false, bool CAUSAL = false, bool Q8 = false>
 __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(const u16* __restrict__ qkv,
                                                                                 u16* __restrict__ out, int N, int H,
@@ -224,13 +229,13 @@ __global__ __launch_bounds__(64 * QW, SINGLE ? 6 : 2) void attention_v2_kernel(c
         }
     } else if (q < N) {
         const float inv = 1.0f / l_run;
-        u16* orow = out + (base + q) * D + h * 64;
+        const size_t orow = ((base + q) * D + h * 64) * 2;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             uint2 w;
             w.x = pack2<T>(o[dt][0] * inv, o[dt][1] * inv);
             w.y = pack2<T>(o[dt][2] * inv, o[dt][3] * inv);
-            *(uint2*)(orow + dt * 16 + 4 * g) = w;
+            gst<ATT_AUX_ST>(out, orow + (dt * 16 + 4 * g) * 2, w);
         }
     }
 }

@@ -1251,9 +1251,10 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
         ok = parse_int(v, x);
         if (ok) h->split_min = x <= 0 ? SPLIT_NEVER : x;
     } else if (k == "gemm_xcd") ok = parse_list(v, h->xcd, 5);
-    else if (k == "qkv_variant" || k == "fc_variant") {  // 100 * XCD map + tile of the QKV / c_fc role,
-        ok = parse_int(v, x) && x > 0;                    // shape rules kept (gemm_variants forces all)
-        const int r = k == "qkv_variant" ? R_QKV : R_FC;
+    else if (k == "qkv_variant" || k == "fc_variant" || k == "out_variant" || k == "proj_variant") {
+        // 100 * XCD map + tile of one role, the shape rules kept (gemm_variants forces all)
+        ok = parse_int(v, x) && x > 0;
+        const int r = k == "qkv_variant" ? R_QKV : k == "fc_variant" ? R_FC : k == "out_variant" ? R_OUT : R_PROJ;
         if (ok) {
             h->var[r] = x % 100;
             h->xcd[r] = x / 100;
@@ -1742,7 +1743,7 @@ int clipvit_gemm_test(void* stream, int dtype, const void* A_dev, const void* W_
     // 16-bit-output-only variants (81 / 82 / 98 LDS-staged; 62, 72-77 persistent), or epi 10 / 11 = 16-bit STORE / GELU on
     // any variant: run, then widen to fp32
     const bool staged = variant == 81 || variant == 82 || variant == 98 || variant == 62 || variant == 72 ||
-                        variant == 74 || variant == 75 || variant == 77;
+                        variant == 74 || variant == 75 || variant == 77 || variant == 79;
     if (epi >= 20) {  // split-K into epi - 20 slices: C_dev = [S][M][N] fp32 partials, no bias
         a.ksplit = epi - 20;
         a.bias = nullptr;

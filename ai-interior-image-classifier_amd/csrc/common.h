@@ -150,9 +150,33 @@ __device__ __forceinline__ void cstore16(void* C, size_t off, const uint4& v) {
     if constexpr (AUX == 0) *(uint4*)((unsigned char*)C + off) = v;
     else st16_pol<AUX>(buf_rsrc(C, 0xFFFFFFFFu), off, v);
 }
-// store policy of the ping-pong (gemm_pp.hip) and MX-fp8 (mx8.hip, gemm_p32mx.h) tiles
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+__device__ void raw_buffer_store_v2i32(i32x2_t data, i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v2i32");
+__device__ void raw_buffer_store_i32(int data, i32x4_t rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.i32");
+// 4-, 8- or 16-byte store at byte offset off (< 4 GB) of the wave-uniform base, cache policy AUX
+// (0: a plain global store)
+template <int AUX, typename V>
+__device__ __forceinline__ void gst(void* base, size_t off, const V& v) {
+    if constexpr (AUX == 0) {
+        *(V*)((unsigned char*)base + off) = v;
+    } else {
+        const i32x4_t rs = buf_rsrc(base, 0xFFFFFFFFu);
+        if constexpr (sizeof(V) == 16) raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, v), rs, (int)(unsigned)off, 0, AUX);
+        else if constexpr (sizeof(V) == 8) raw_buffer_store_v2i32(__builtin_bit_cast(i32x2_t, v), rs, (int)(unsigned)off, 0, AUX);
+        else raw_buffer_store_i32(__builtin_bit_cast(int, v), rs, (int)(unsigned)off, 0, AUX);
+    }
+}
+// store policy of the streaming kernels' outputs (LayerNorm x / h, attention, im2col)
+#ifndef EW_AUX_ST
+#define EW_AUX_ST 0
+#endif
+// store policy of the ping-pong (gemm_pp.hip: sc0 sc1, B/32 bs 128 +2.2 % same box, c_fc 0.48 ->
+// 0.445 ms per forward) and MX-fp8 (mx8.hip, gemm_p32mx.h: plain; sc0 sc1 measured -6 % on config
+// 5) tiles (profiles/r06/store_policy_ab.txt)
 #ifndef PP_AUX_ST
-#define PP_AUX_ST 0
+#define PP_AUX_ST GEMM_ST_AUX
 #endif
 #ifndef MX_AUX_ST
 #define MX_AUX_ST 0
@@ -277,9 +301,9 @@ __device__ __forceinline__ float4 x24_load(const unsigned char* base, size_t pla
 __device__ __forceinline__ void x24_store(unsigned char* base, size_t plane, size_t idx, float4 v) {
     const unsigned a = __float_as_uint(v.x) + 0x80u, b = __float_as_uint(v.y) + 0x80u;
     const unsigned c = __float_as_uint(v.z) + 0x80u, d = __float_as_uint(v.w) + 0x80u;
-    *(uint2*)(base + idx * 2) = make_uint2((a >> 16) | (b & 0xffff0000u), (c >> 16) | (d & 0xffff0000u));
-    *(unsigned*)(base + plane + idx) =
-        ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c << 8) & 0xff0000u) | ((d << 16) & 0xff000000u);
+    gst<EW_AUX_ST>(base, idx * 2, make_uint2((a >> 16) | (b & 0xffff0000u), (c >> 16) | (d & 0xffff0000u)));
+    gst<EW_AUX_ST>(base, plane + idx,
+                   ((a >> 8) & 0xffu) | (b & 0xff00u) | ((c << 8) & 0xff0000u) | ((d << 16) & 0xff000000u));
 }
 
 // mean / rstd of a row from its np (mean, M2) partials over 128 columns each (Chan's combine,

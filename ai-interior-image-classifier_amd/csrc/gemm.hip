@@ -326,10 +326,11 @@ __device__ __forceinline__ void res_stats_epilogue(const GemmArgs& a, f32x4 (&ac
 }
 
 // SM = 3: 16-bit outputs are staged through LDS and stored as whole rows (see the epilogue).
-// C stores of the pipelined tiles' epilogues (16-bit C, the patch rows): cache policy PIPE_AUX_ST
-// (0 = plain global stores; otherwise buffer stores over C with those policy bits; default sc0
-// sc1, common.h GEMM_ST_AUX). r06 same box, B/32 bs 256: out_proj 0.245 -> 0.225 ms, c_proj
-// 0.665 -> 0.658 ms per forward, +1.1 % against plain stores (profiles/r06/store_policy_ab.txt)
+// 16-bit C stores of the pipelined tiles' epilogues: cache policy PIPE_AUX_ST (0 = plain global
+// stores; otherwise buffer stores over C with those policy bits; default sc0 sc1, common.h
+// GEMM_ST_AUX). r06 same box, B/32 bs 256: out_proj 0.245 -> 0.225 ms, c_proj 0.665 -> 0.658 ms
+// per forward, +1.1 % against plain stores; the patch GEMM's fp32 rows stay plain (sc0 sc1 there:
+// patch family 0.12 -> 0.15 ms; profiles/r06/store_policy_ab.txt)
 #ifndef PIPE_AUX_ST
 #define PIPE_AUX_ST GEMM_ST_AUX
 #endif
@@ -757,11 +758,8 @@ __global__ __launch_bounds__(64 * WM* WN, WM* WN >= 4 ? 2 : 4) void gemm_pipe_ke
                     row = (size_t)(m / a.patch_g2) * a.patch_ntok + 1 + (m % a.patch_g2);
                 const size_t off = (row * a.ldc + n) * 4;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float4 o = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-                    if constexpr (EPI == EPI_PATCH) cstore16<PIPE_AUX_ST>(Cb, off + 16 * i, __builtin_bit_cast(uint4, o));
-                    else *(float4*)(Cb + off + 16 * i) = o;
-                }
+                for (int i = 0; i < 4; ++i)
+                    *(float4*)(Cb + off + 16 * i) = (make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]));
             }
         }
     }
@@ -893,14 +891,14 @@ static int launch_t(hipStream_t s, int epi, const GemmArgs& a, int variant) {
 
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant) {
     if (a.K % 64 != 0 || a.M <= 0) return -1;
-    if (a.blk_a || a.blk_c) {  // blocked u / h: pipelined 8..98 and persistent 62 / 72 / 74 / 75 / 77 only
+    if (a.blk_a || a.blk_c) {  // blocked u / h: pipelined 8..98 and persistent 62 / 72 / 74 / 75 / 77 / 79 only
         if (variant < 8 || a.ksplit > 1) return -1;
         if (a.blk_c && (a.ldc % 64 || (epi != EPI_STORE && epi != EPI_GELU && epi != EPI_LNF && epi != EPI_LNF_GELU)))
             return -1;
     }
-    // blocked W: the pipelined tiles and the persistent tiles (62 / 72 / 74 / 75 / 77)
+    // blocked W: the pipelined tiles and the persistent tiles (62 / 72 / 74 / 75 / 77 / 79)
     if (a.blk_w && (variant < 8 || a.ksplit > 1)) return -1;
-    if (variant == 62 || variant == 72 || variant == 74 || variant == 75 || variant == 77)
+    if (variant == 62 || variant == 72 || variant == 74 || variant == 75 || variant == 77 || variant == 79)
         return launch_gemm_pp(s, dtype, epi, a, variant);
     // split-K runs on the pipelined tiles only (launch_pipe checks the epilogue and K)
     if (a.ksplit > 1 && variant < 8) return -1;

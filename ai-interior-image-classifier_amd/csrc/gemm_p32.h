@@ -80,13 +80,14 @@ struct P32NoHooks {
 
 // NT: non-temporal epilogue stores (variant 74: the large-M c_fc, whose u would otherwise sit
 // dirty in the L2 / Infinity Cache in front of the next blocks' operands)
-// BM: tile rows, 256 or 320 (variant 77: 320 x 256 tiles, each wave 160 x 64; FM = BM / 32
+// BM: tile rows, 192, 256 or 320 (variant 79: 192 x 256, each wave 96 x 64; variant 77: 320 x
+// 256 tiles, each wave 160 x 64; FM = BM / 32
 // accumulator fragments per column slice, NP = the wave's LDS-DMA pieces per k-step: BM / 64
 // for group 0 (A), 4 for group 1 (W))
 template <typename T, int EPI, bool BLKA, bool BLKW, int GRP, bool NT, int BM, class HK>
 __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned char* smem, int lane, int wc, HK& hk) {
     typedef typename T::vec8 vec8;
-    static_assert(BM == 256 || BM == 320, "p32 tile rows");
+    static_assert(BM == 192 || BM == 256 || BM == 320, "p32 tile rows");
     constexpr int BN = 256;
     constexpr int A_ST = BM * 64, STAGE = (BM + BN) * 64;  // 16 / 20 KB + 16 KB
     constexpr int FM = BM / 32, NP = GRP == 0 ? BM / 64 : 4, HALF = BM / 2;
@@ -191,8 +192,10 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
         rd(af[3], ba, std::integral_constant<int, SO + 3 * AFSTEP>{});
         rd(af[4], ba, std::integral_constant<int, SO + 4 * AFSTEP>{});
         rd(af[5], ba, std::integral_constant<int, SO + 5 * AFSTEP>{});
-        rd(af[6], ba, std::integral_constant<int, SO + 6 * AFSTEP>{});
-        rd(af[7], ba, std::integral_constant<int, SO + 7 * AFSTEP>{});
+        if constexpr (FM > 6) {
+            rd(af[6 % FM], ba, std::integral_constant<int, SO + 6 * AFSTEP>{});
+            rd(af[7 % FM], ba, std::integral_constant<int, SO + 7 * AFSTEP>{});
+        }
         if constexpr (FM > 8) {
             rd(af[8 % FM], ba, std::integral_constant<int, SO + 8 * AFSTEP>{});
             rd(af[9 % FM], ba, std::integral_constant<int, SO + 9 * AFSTEP>{});
@@ -294,10 +297,9 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
     // counts and the code are the same.
     constexpr int W_LO = 2 * NP, W_HI = 2 * NP + 2 * FM;
     const i32x4_t rs_drop = buf_rsrc(a.C, 0u);
-    auto null_stores = [&]() {  // inline asm: hipcc would merge 16 identical stores into one
+    auto null_stores = [&]() {  // inline asm: hipcc would merge the 2 FM identical stores into one
         const u32x4 z = {0u, 0u, 0u, 0u};
         asm volatile(
-            "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
             "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
             "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
             "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
@@ -308,6 +310,14 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
             :
             : "v"(z), "s"(rs_drop)
             : "memory");
+        if constexpr (FM > 6) {
+            asm volatile(
+                "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
+                "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0"
+                :
+                : "v"(z), "s"(rs_drop)
+                : "memory");
+        }
         if constexpr (FM > 8) {
             asm volatile(
                 "buffer_store_dwordx4 %0, off, %1, 0\n\tbuffer_store_dwordx4 %0, off, %1, 0\n\t"
@@ -420,7 +430,7 @@ __device__ __forceinline__ void p32_body(const GemmArgs& a, int ntiles, unsigned
 }
 
 // LDS: four stages of (BM + 256) x 64 B, then the GEMM's bias vector (fp32): 160 KB in all, so
-// N <= 8192 at BM = 256 and N <= 4096 at BM = 320 (launch_p32_t checks)
+// N <= 8192 at BM = 192 / 256 and N <= 4096 at BM = 320 (launch_p32_t checks)
 template <typename T, int EPI, bool BLKA, bool BLKW = false, bool NT = false, int BM = 256, class HK = P32NoHooks>
 __global__ __launch_bounds__(512, 1) void gemm_p32_kernel(GemmArgs a, int ntiles) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[4 * 512 * 64 + 8192 * 4];  // 160 KB

@@ -326,7 +326,7 @@ static int launch_ppp_t(hipStream_t s, int epi, const GemmArgs& a) {
 template <typename T, bool BLKW, bool NT, int BM = 256>
 static int launch_p32_t(hipStream_t s, int epi, const GemmArgs& a, bool balanced = false) {
     if (a.K % 128 || a.K < 256) return -1;  // whole groups of four 32-deep k-steps, >= 2 groups
-    if (a.N > (BM == 256 ? 8192 : 4096)) return -1;  // the bias vector's LDS room (gemm_p32_kernel)
+    if (a.N > (BM <= 256 ? 8192 : 4096)) return -1;  // the bias vector's LDS room (gemm_p32_kernel)
     if ((size_t)(a.M + 15) * a.ldc * 2 >= 0xFFFFFFF0u) return -1;  // C offsets are 32-bit (gemm_p32.h rs_out)
     const int ncu = a.ncu > 0 ? a.ncu : 256;
     const int ntiles = ((a.M + BM - 1) / BM) * (a.N / 256);
@@ -356,6 +356,15 @@ static int launch_p32_320(hipStream_t s, int epi, const GemmArgs& a) {
     return a.blk_w ? launch_p32_t<T, true, false, 320>(s, epi, a, true) : launch_p32_t<T, false, false, 320>(s, epi, a, true);
 }
 
+// variant 79: 192 x 256 tiles on a balanced grid, for the N = 768 roles (out_proj, c_proj at
+// B/32 bs 256: 67 x 3 = 201 tiles, one per workgroup): one workgroup stages its A rows once for
+// 256 columns, where two 160 x 128 workgroups on a CU stage theirs twice (22 % fewer staged bytes
+// per CU than variant 82)
+template <typename T>
+static int launch_p32_192(hipStream_t s, int epi, const GemmArgs& a) {
+    return a.blk_w ? launch_p32_t<T, true, false, 192>(s, epi, a, true) : launch_p32_t<T, false, false, 192>(s, epi, a, true);
+}
+
 // variant 62: persistent ping-pong (direct stores; 1-D XCD maps only, N <= 8192); 63: 62 with
 // non-temporal stores (the large-M roles of B/16 and L/14@336); 72: the 32-deep-k-step
 // persistent tile of gemm_p32.h; 74: 72 with non-temporal stores; 75: 72 on a balanced grid (600
@@ -371,6 +380,8 @@ int launch_gemm_pp(hipStream_t s, int dtype, int epi, const GemmArgs& a, int var
         return dtype == 2 ? launch_p32<F16>(s, epi, a, false, true) : launch_p32<BF16>(s, epi, a, false, true);
     if (variant == 77)  // 320 x 256 tiles, balanced grid
         return dtype == 2 ? launch_p32_320<F16>(s, epi, a) : launch_p32_320<BF16>(s, epi, a);
+    if (variant == 79)  // 192 x 256 tiles, balanced grid
+        return dtype == 2 ? launch_p32_192<F16>(s, epi, a) : launch_p32_192<BF16>(s, epi, a);
     return -1;
 }
 

@@ -40,8 +40,8 @@ __global__ void cast_pixels_kernel(const void* __restrict__ src, u16* __restrict
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = IN == 1 ? BF16::to_f32(hv[e]) : F16::to_f32(hv[e]);
     }
-    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                                  pack2<TO>(v[6], v[7]));
+    gst<EW_AUX_ST>(dst, (size_t)i * 16, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                                 pack2<TO>(v[6], v[7])));
 }
 
 template <typename TO>
@@ -84,8 +84,8 @@ __global__ void cast_pixels_padded_kernel(const void* __restrict__ src, u16* __r
         const int j = j0 + e;
         v[e] = j < P ? load_pix<IN>(src, (size_t)row * R + px * P + j) : 0.f;
     }
-    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                                  pack2<TO>(v[6], v[7]));
+    gst<EW_AUX_ST>(dst, (size_t)i * 16, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                                 pack2<TO>(v[6], v[7])));
 }
 
 void launch_cast_pixels_padded(hipStream_t s, int in_dtype, int out_dtype, const void* src, void* dst, int B,
@@ -145,8 +145,8 @@ __global__ void im2col_blk_kernel(const void* __restrict__ src, u16* __restrict_
                 if (j0 + e < P) v[e] = load_pix<IN>(src, base + e);
         }
     }
-    ((uint4*)dst)[i] = make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
-                                  pack2<TO>(v[6], v[7]));
+    gst<EW_AUX_ST>(dst, (size_t)i * 16, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]),
+                                                 pack2<TO>(v[6], v[7])));
 }
 
 template <typename TO, int IN>
@@ -481,14 +481,16 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(void* __restrict__ x
         __syncthreads();
         unsigned char* dst = (unsigned char*)h + (size_t)blockIdx.x * 32 * D;
         for (int o = threadIdx.x * 16; o < 32 * D; o += 256 * 16)
-            *(uint4*)(dst + o) = *(const uint4*)(hs + hblk_lds_off(o >> 11, (o >> 8) & 7, (o >> 4) & 15));
+            gst<EW_AUX_ST>(h, (size_t)(dst - (unsigned char*)h) + o,
+                           *(const uint4*)(hs + hblk_lds_off(o >> 11, (o >> 8) & 7, (o >> 4) & 15)));
     } else if constexpr (HBLK == 3) {  // 16 D bytes as 128-B runs: rows m0..m0+7 of each (block, chunk)
         __syncthreads();
         const int m0 = blockIdx.x * 8;
         unsigned char* dst = (unsigned char*)h + (size_t)(m0 >> 4) * 32 * D + (m0 & 15) * 16;
         for (int o = threadIdx.x * 16; o < 16 * D; o += 256 * 16) {
             const int run = o >> 7, b = run >> 3, c = run & 7, m = (o >> 4) & 7;
-            *(uint4*)(dst + b * 2048 + c * 256 + m * 16) = *(const uint4*)(hs + hblk8_lds_off(b, c, m));
+            gst<EW_AUX_ST>(h, (size_t)(dst - (unsigned char*)h) + b * 2048 + c * 256 + m * 16,
+                           *(const uint4*)(hs + hblk8_lds_off(b, c, m)));
         }
     }
 }

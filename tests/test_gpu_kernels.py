@@ -32,13 +32,14 @@ def _ref_gemm(A, W, bias, epi, C0=None):
 # 98 240x256 (12 waves), 90 64x64 (class-token tail), 62 the persistent 256x256 ping-pong tile
 # (gemm_pp.hip; 72 the 32-deep-k-step persistent tile of
 # gemm_p32.h; 74 the same with non-temporal stores; 75 on a balanced grid; 77 its 320 x 256 form on a balanced
-# grid); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
+# grid; 79 its 192 x 256 form on a balanced grid); + 10000 = W in the 16-row blocked layout (GemmArgs.blk_w, tuning w_blocked);
 # 2xx = the production XCD partition.
-VARIANTS = [1, 2, 3, 8, 22, 62, 72, 74, 75, 77, 81, 82, 90, 98, 208, 222, 282, 298, 3408, 3462, 3472,
-            3474, 3477, 10008, 10022, 10062, 10072, 10077, 10081, 10082, 10090, 10098, 13462, 13472, 13477]
+VARIANTS = [1, 2, 3, 8, 22, 62, 72, 74, 75, 77, 79, 81, 82, 90, 98, 208, 222, 282, 298, 3408, 3462, 3472,
+            3474, 3477, 3479, 10008, 10022, 10062, 10072, 10077, 10079, 10081, 10082, 10090, 10098, 13462, 13472,
+            13477, 13479]
 N128 = (1, 2, 22, 81, 82)
-N256 = (3, 8, 62, 72, 74, 75, 77, 98)
-STAGED = (62, 72, 74, 75, 77, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
+N256 = (3, 8, 62, 72, 74, 75, 77, 79, 98)
+STAGED = (62, 72, 74, 75, 77, 79, 81, 82, 98)  # 16-bit outputs only (rounded to 16 bits)
 
 
 def _tol(variant, dtype):
@@ -55,7 +56,7 @@ def _skip(variant, N, K):
         return "tile does not divide N"
     if v in (62, 63) and K % 128:
         return "ping-pong tile: K in pairs of 64-deep k-tiles"
-    if v in (72, 74, 75, 77) and (K % 128 or K < 256):
+    if v in (72, 74, 75, 77, 79) and (K % 128 or K < 256):
         return "32-deep-k-step tile: K a multiple of 128, >= 256"
     return None
 
@@ -78,7 +79,7 @@ def test_gemm_shapes(gpu, dtype, variant, M, N, K):
     assert err < _tol(variant, dtype), err
 
 
-@pytest.mark.parametrize("variant", STAGED + (8, 22, 10072, 10077, 10081, 10098))
+@pytest.mark.parametrize("variant", STAGED + (8, 22, 10072, 10077, 10079, 10081, 10098))
 @pytest.mark.parametrize("epi", [10, 11])
 def test_gemm_staged_16bit_epilogue(gpu, variant, epi):
     """16-bit STORE / GELU epilogues on ragged M (last tile partial): LDS-staged row-contiguous
@@ -239,7 +240,7 @@ def test_attention_persistent_bit_identical(gpu, dtype, B, N, H, persist):
         assert torch.equal(out, ref), (rep, (out.float() - ref.float()).abs().max().item())
 
 
-@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
+@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072), (12800, 768, 3072),
                                    (36928 // 4, 4096, 1024)])
 def test_ping_pong_race_screen(gpu, M, N, K):
     """The persistent ping-pong GEMM (62; + 10000 with the blocked weight copy) hands LDS stages between waves by counted vmcnt and
@@ -258,7 +259,7 @@ def test_ping_pong_race_screen(gpu, M, N, K):
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
 
 
-@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072),
+@pytest.mark.parametrize("M,N,K", [(12800, 3072, 768), (10752, 3072, 768), (1000, 2304, 768), (333, 768, 3072), (12800, 768, 3072),
                                    (36928 // 4, 4096, 1024), (50432, 2304, 768)])
 def test_p32_race_screen(gpu, M, N, K):
     """The 32-deep-k-step persistent tiles (72 / 74 non-temporal / 75 on the balanced grid / 77 its 320 x 256 form; the large-M roles' and the B/32
@@ -274,7 +275,7 @@ def test_p32_race_screen(gpu, M, N, K):
     bias = torch.randn(N, device=gpu, generator=g)
     for epi in (10, 11):  # 16-bit store / QuickGELU
         ref = E.gemm_test(A, W, bias, epi=epi, variant=8)
-        for variant in (72, 3472, 10072, 13472, 74, 13474, 10075, 77, 3477, 10077, 13477):
+        for variant in (72, 3472, 10072, 13472, 74, 13474, 10075, 77, 3477, 10077, 13477, 79, 10079, 13479):
             for _ in range(4):
                 C = E.gemm_test(A, W, bias, epi=epi, variant=variant)
                 assert torch.equal(C, ref), (variant, epi, (C - ref).abs().max().item())
@@ -305,7 +306,7 @@ def test_residual_x24_round_trip(gpu):
     assert rel <= 2.0 ** -16, rel
 
 
-@pytest.mark.parametrize("variant", [8, 22, 62, 72, 75, 77, 81, 82, 98, 298, 3475, 3477])
+@pytest.mark.parametrize("variant", [8, 22, 62, 72, 75, 77, 79, 81, 82, 98, 298, 3475, 3477, 3479])
 @pytest.mark.parametrize("M,N,K", [(1000, 2304, 768), (12800, 3072, 768)])
 def test_blocked_a_is_bit_identical(gpu, variant, M, N, K):
     """A (the LayerNorm output h that QKV / c_fc read) in the 16-row blocked layout (+ 20000; with
