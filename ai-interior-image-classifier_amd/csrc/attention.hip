@@ -46,7 +46,8 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // `out`: each value rounded to T first, then quantized by the launch_quant_mx8 rule, so the bytes
 // equal attention + quant_mx8 exactly. MX block b of a head = features 32 b .. 32 b + 31 = the
 // lane's dt 2b, 2b+1 values across the 4 lanes of its query (g = 0..3).
-// store policy of the attention output (common.h gst; 0 = plain stores)
+// store policy of the attention output (common.h gst; 0 = plain stores; sc0 sc1 measured
+// slower: attention family 0.20 -> 0.22 ms per forward, profiles/r06/store_policy_ab.txt)
 #ifndef ATT_AUX_ST
 #define ATT_AUX_ST 0
 #endif

@@ -168,9 +168,12 @@ __device__ __forceinline__ void gst(void* base, size_t off, const V& v) {
         else raw_buffer_store_i32(__builtin_bit_cast(int, v), rs, (int)(unsigned)off, 0, AUX);
     }
 }
-// store policy of the streaming kernels' outputs (LayerNorm x / h, attention, im2col)
+// store policy of the streaming kernels' outputs (the 24-bit residual planes, the LayerNorm
+// kernels' blocked h, im2col): sc0 sc1. r06 same box, B/32 bs 256: LayerNorm family 0.366-0.372
+// -> 0.351-0.359 ms per forward, +0.4-0.9 % (the attention output measured slower that way:
+// attention.hip ATT_AUX_ST; profiles/r06/store_policy_ab.txt)
 #ifndef EW_AUX_ST
-#define EW_AUX_ST 0
+#define EW_AUX_ST GEMM_ST_AUX
 #endif
 // store policy of the ping-pong (gemm_pp.hip: sc0 sc1, B/32 bs 128 +2.2 % same box, c_fc 0.48 ->
 // 0.445 ms per forward) and MX-fp8 (mx8.hip, gemm_p32mx.h: plain; sc0 sc1 measured -6 % on config
