@@ -184,6 +184,9 @@ __device__ __forceinline__ void gst(void* base, size_t off, const V& v) {
 #ifndef MX_AUX_ST
 #define MX_AUX_ST 0
 #endif
+#ifndef MX_AUX_ST16  // the MX tiles' 16-bit / fp32 outputs (MX_AUX_ST: their MX-fp8 outputs)
+#define MX_AUX_ST16 0
+#endif
 
 // ---- MX-fp8: OCP e4m3 elements, one E8M0 (power-of-two) scale per 32 consecutive K ----
 // Block rule (shared by every producer and by the tests' host reference): e = the smallest

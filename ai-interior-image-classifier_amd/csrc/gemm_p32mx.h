@@ -252,13 +252,13 @@ __device__ __forceinline__ void p32mx_body(const GemmArgs& a, int ntiles, unsign
 #pragma unroll
                     for (int i = 0; i < 4; ++i)
                         raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, f32x4{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]}),
-                                               rs_out, (int)(off + 16u * i), 0, 0);
+                                               rs_out, (int)(off + 16u * i), 0, MX_AUX_ST16);
                 } else {
                     const u32x4 w0 = {pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]), pack2<TO>(v[4], v[5]), pack2<TO>(v[6], v[7])};
                     const u32x4 w1 = {pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]), pack2<TO>(v[12], v[13]), pack2<TO>(v[14], v[15])};
                     const unsigned off = m < a.M ? ((unsigned)m * (unsigned)a.ldc + (unsigned)n) * 2u : 0xFFFFFFE0u;
-                    raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w0), rs_out, (int)off, 0, MX_AUX_ST);
-                    raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w1), rs_out, (int)(off + 16u), 0, MX_AUX_ST);
+                    raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w0), rs_out, (int)off, 0, MX_AUX_ST16);
+                    raw_buffer_store_v4i32(__builtin_bit_cast(i32x4_t, w1), rs_out, (int)(off + 16u), 0, MX_AUX_ST16);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // one block at a time (register pressure)
             }

@@ -747,9 +747,9 @@ __global__ __launch_bounds__(512, 1) void gemm_mx8_pp_kernel(GemmArgs a, int nti
                 }
             } else if (m < a.M) {  // EPI_STORE
                 const size_t off = ((size_t)m * a.ldc + n) * 2;
-                cstore16<MX_AUX_ST>(a.C, off, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]),
+                cstore16<MX_AUX_ST16>(a.C, off, make_uint4(pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3]),
                                                          pack2<TO>(v[4], v[5]), pack2<TO>(v[6], v[7])));
-                cstore16<MX_AUX_ST>(a.C, off + 16, make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]),
+                cstore16<MX_AUX_ST16>(a.C, off + 16, make_uint4(pack2<TO>(v[8], v[9]), pack2<TO>(v[10], v[11]),
                                                               pack2<TO>(v[12], v[13]), pack2<TO>(v[14], v[15])));
             }
         }
