@@ -266,7 +266,7 @@ def parity_config5(eng, px, T_rand, cfg, dev, n: int = 64, n_oracle: int = 4):
     return out
 
 
-DEFAULT_PROFILE = ROOT / "profiles" / "r06b_fc_traffic.json"  # committed by tools/profile_round.sh
+DEFAULT_PROFILE = ROOT / "profiles" / "r06c_fc_traffic.json"  # committed by tools/profile_round.sh
 
 
 def load_traffic(path: str | None):
