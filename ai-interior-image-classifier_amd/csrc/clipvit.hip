@@ -251,6 +251,10 @@ struct clipvit_handle {
     // MX-fp8 forward: attention writes the out_proj operand (MX-fp8) itself instead of 16-bit
     // output + launch_quant_mx8 (same bytes; tuning attn_q8=0 restores the two kernels)
     bool attn_q8 = true;
+    // ViT-B/32 on the 24-bit residual path: attention + out_proj + (x += y) + ln_2 of blocks
+    // 0 .. L-2 as one kernel per image (attn_block.hip; tuning attn_fuse=1).
+    // Measured slower than the three kernels (B/32 88.5-88.8k -> 81.6-82.1k img/s same box), so off
+    bool attn_fuse = false;
     bool round_split = true;
     // tiles of the two launches (0 = the role's); tuning split_variants. r05: 72 as the main
     // launch measured +0.3-0.6 % with the bias as its first MFMA's C (profiles/r05/
@@ -969,15 +973,21 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                        hq && i > 0)))
             return rc;
         if (prof) prof->mark(s, F_QKV);
-        launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
+        const bool defer = h->resid16 && h->defer_x && !last;
+        // blocks 0 .. L-2 of ViT-B/32: attention, out_proj, x += y and ln_2 in one kernel per image
+        // (x then already holds x + y, so the ln_1 below adds only c_proj's y2)
+        const bool fused = h->attn_fuse && defer && X24 && hb != 0 &&
+                           launch_attn_out_ln(s, h->dt, w->qkv, ly.wout_b, ly.bout, X24, (size_t)M * D * 2, ly.ln2g,
+                                              ly.ln2b, w->h, B, N, D) == 0;
+        if (!fused) launch_attention(s, h->dt, w->qkv, w->h, B, N, h->cfg.heads, false, h->attn_persist, h->ncu);
         if (prof) prof->mark(s, F_ATTN);
         if (last && h->cls_prune) {
             if ((rc = cls_tail(h, s, B, w, f_out, prof, X24, X24 != nullptr))) return rc;
             HIPCHK(hipGetLastError());
             return 0;
         }
-        const bool defer = h->resid16 && h->defer_x && !last;
-        if (h->resid16) {
+        if (fused) {
+        } else if (h->resid16) {
             if ((rc = gemm(s, h, EPI_STORE, w->h, ly.wout, ly.bout, y, M, D, D, D, R_OUT, Fold(), w, ly.wout_b))) return rc;
             if (prof) prof->mark(s, F_OUT);
             if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, nullptr, w->h, ly.ln2g, ly.ln2b, M, D, X24, X24 != nullptr, hb);
@@ -997,8 +1007,9 @@ static int forward(clipvit_handle* h, hipStream_t s, const void* pix, int in_dty
                 return rc;
             if (prof) prof->mark(s, F_PROJ);
             const LayerW& nx = h->layers[i + 1];
-            if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr,
-                                                     hq ? 3 : X24 && h->ln1_rows == 2 ? 4 : 0);
+            if (fused) launch_add_layernorm_x24_store(s, h->dt, X24, y2, w->h, nx.ln1g, nx.ln1b, M, D, hq ? 3 : 0);
+            else if (defer) launch_add_layernorm_deferred(s, h->dt, w->x, y, y2, w->h, nx.ln1g, nx.ln1b, M, D, X24, X24 != nullptr,
+                                                          hq ? 3 : X24 && h->ln1_rows == 2 ? 4 : 0);
             else launch_add_layernorm(s, h->dt, w->x, y, w->h, nx.ln1g, nx.ln1b, M, D);
             if (prof) prof->mark(s, F_LN);
         } else {
@@ -1225,6 +1236,7 @@ static int apply_tuning(clipvit_handle* h, const std::string& k, const std::stri
     else if (k == "fc_balanced") ok = flag(h->fc_balanced);
     else if (k == "fc_balanced_variant") ok = parse_int(v, h->fc_bal_var) && (h->fc_bal_var == 75 || h->fc_bal_var == 77);
     else if (k == "attn_q8") ok = flag(h->attn_q8);
+    else if (k == "attn_fuse") ok = flag(h->attn_fuse);
     else if (k == "x16") ok = flag(h->x16);
     else if (k == "x24") ok = flag(h->x24);
     else if (k == "u_blocked") ok = flag(h->u_blk);
@@ -1295,14 +1307,14 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
     }
     // a bad item leaves the handle as it was: apply to a snapshot of the tunable fields first
     struct Tun {
-        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace;
+        bool resid16, defer_x, lnfold, cls_prune, round_split, attn_q8, x16, x24, var_forced, u_blk, fc_balanced, trace, attn_fuse;
         int h_blk, patch_im2col, ln1_rows, qkv_blk, attn_persist, w_blk, fc_bal_var, split_main, split_tail, tail_var, tail_kmin, tail_smax, head_cols, split_xcd, max_inflight, split_min, mx8_split_tail;
         int xcd[5], var8[4], large_var[4], var[5];
         uint64_t mx8_skip, mx8_skip_mlp;
     };
     auto save = [](const clipvit_handle* g) {
         Tun t{g->resid16, g->defer_x, g->lnfold, g->cls_prune, g->round_split, g->attn_q8, g->x16, g->x24,
-              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->h_blk, g->patch_im2col, g->ln1_rows, g->qkv_blk, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
+              g->var_forced, g->u_blk, g->fc_balanced, g->trace, g->attn_fuse, g->h_blk, g->patch_im2col, g->ln1_rows, g->qkv_blk, g->attn_persist, g->w_blk, g->fc_bal_var, g->split_main, g->split_tail, g->tail_var, g->tail_kmin, g->tail_smax, g->head_cols,
               g->split_xcd, g->max_inflight,
               g->split_min, g->mx8_split_tail, {}, {}, {}, {}, g->mx8_skip, g->mx8_skip_mlp};
         memcpy(t.xcd, g->xcd, sizeof t.xcd);
@@ -1318,7 +1330,7 @@ int clipvit_set_tuning(clipvit_handle* h, const char* spec) {
             h->resid16 = before.resid16; h->defer_x = before.defer_x; h->lnfold = before.lnfold;
             h->cls_prune = before.cls_prune; h->round_split = before.round_split; h->attn_q8 = before.attn_q8;
             h->x16 = before.x16; h->x24 = before.x24; h->var_forced = before.var_forced; h->u_blk = before.u_blk;
-            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->ln1_rows = before.ln1_rows; h->qkv_blk = before.qkv_blk; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
+            h->fc_balanced = before.fc_balanced; h->trace = before.trace; h->attn_fuse = before.attn_fuse; h->h_blk = before.h_blk; h->patch_im2col = before.patch_im2col; h->ln1_rows = before.ln1_rows; h->qkv_blk = before.qkv_blk; h->attn_persist = before.attn_persist; h->w_blk = before.w_blk; h->fc_bal_var = before.fc_bal_var;
             h->split_main = before.split_main; h->split_tail = before.split_tail; h->tail_var = before.tail_var;
             h->tail_kmin = before.tail_kmin; h->tail_smax = before.tail_smax; h->head_cols = before.head_cols;
             h->split_xcd = before.split_xcd; h->max_inflight = before.max_inflight; h->split_min = before.split_min;

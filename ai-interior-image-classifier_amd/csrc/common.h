@@ -416,6 +416,12 @@ __device__ __forceinline__ void store_row16(u16* dst, const float4 (&v)[V], int 
 }
 
 // ---- launchers (defined in the .hip translation units) ----
+// attention + out_proj + (x += y) + ln_2 of one block, one workgroup per image (attn_block.hip);
+// -1 when the shape is not covered (D != 768, N > 64, no blocked W_out copy)
+int launch_attn_out_ln(hipStream_t s, int dtype, const void* qkv, const void* wout_blk, const float* bout,
+                       void* x24, size_t plane, const float* g2, const float* b2, void* h, int B, int N, int D);
+void launch_add_layernorm_x24_store(hipStream_t s, int dtype, void* x24, const void* y, void* h, const float* g,
+                                    const float* b, int rows, int D, int hblk);
 // variant: 0 = auto by shape; tile variants listed in gemm.hip launch_t
 int launch_gemm(hipStream_t s, int dtype, int epi, const GemmArgs& a, int variant);
 // ping-pong 256x256 GEMM (gemm_pp.hip): variant 60 direct stores, 61 LDS-staged stores;

@@ -703,6 +703,27 @@ void launch_splitk_gelu(hipStream_t s, int dtype, const float* P, int S, const f
     else splitk_gelu_kernel<BF16><<<grid, block, 0, s>>>(P, S, bias, (u16*)u, rows, n);
 }
 
+// x = x + y stored (24-bit planes), h = LayerNorm(x): ln_1 after the fused attention sub-block
+// (attn_block.hip), whose x already holds x + y_out, so only c_proj's y2 is added here. hblk 3:
+// h in the 16-row blocked layout (8-row groups, as the deferred form's), 0: row-major.
+void launch_add_layernorm_x24_store(hipStream_t s, int dtype, void* x24, const void* y, void* h, const float* g,
+                                    const float* b, int rows, int D, int hblk) {
+    const u16* yy = (const u16*)y;
+    if (hblk == 3) {
+        dim3 grid((rows + 15) / 16 * 2), block(256);
+        if (dtype == 2)
+            DISPATCH_V(D, (add_layernorm_kernel<F16, V, true, false, 2, false, false, true, 3><<<grid, block, 0, s>>>(x24, yy, nullptr, h, nullptr, g, b, rows)))
+        else
+            DISPATCH_V(D, (add_layernorm_kernel<BF16, V, true, false, 2, false, false, true, 3><<<grid, block, 0, s>>>(x24, yy, nullptr, h, nullptr, g, b, rows)))
+        return;
+    }
+    dim3 grid((rows + 3) / 4), block(256);
+    if (dtype == 2)
+        DISPATCH_V(D, (add_layernorm_kernel<F16, V, true, false, 1, false, false, true, 0><<<grid, block, 0, s>>>(x24, yy, nullptr, h, nullptr, g, b, rows)))
+    else
+        DISPATCH_V(D, (add_layernorm_kernel<BF16, V, true, false, 1, false, false, true, 0><<<grid, block, 0, s>>>(x24, yy, nullptr, h, nullptr, g, b, rows)))
+}
+
 void launch_add_layernorm_deferred(hipStream_t s, int dtype, float* x, const void* y, const void* y2,
                                    void* h, const float* g, const float* b, int rows, int D, void* x16, bool x24,
                                    int hblk) {

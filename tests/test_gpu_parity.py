@@ -507,7 +507,9 @@ def test_blocked_w_is_bit_identical(gpu, name, dtype, B, tun, fc):
     px = _pixels(B, cfg.image_size, seed=53).to(gpu)
     outs = []
     for blk in (2, 1, 0):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk, trace_gemm=1))
+        # attn_fuse=0: the fused attention sub-block reads only the blocked W_out copy, so the
+        # layouts are compared on the three-kernel path (test_attention_block_fusion covers it)
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, w_blocked=blk, trace_gemm=1, attn_fuse=0))
         try:
             eng.load_state_dict(sd)
             eng.load_lora(ad)
@@ -545,7 +547,8 @@ def test_blocked_h_is_bit_identical(gpu, name, dtype, B, tun, hmode):
     px = _pixels(B, cfg.image_size, seed=59).to(gpu)
     outs = []
     for hb in (hmode, 0):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, h_blocked=hb, trace_gemm=1))
+        # attn_fuse=0: the fused attention sub-block writes blocked h itself (h_blocked != 0 only)
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(tun, h_blocked=hb, trace_gemm=1, attn_fuse=0))
         try:
             eng.load_state_dict(sd)
             eng.load_lora(ad)
@@ -602,7 +605,7 @@ def test_attention_persistent_engine_bit_identical(gpu, dtype, persist):
     px = _pixels(64, cfg.image_size, seed=67).to(gpu)
     outs = []
     for p in (persist, 0):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=64, tuning=dict(attn_persist=p))
+        eng = VisionEngine(cfg, 0, dtype, max_batch=64, tuning=dict(attn_persist=p, attn_fuse=0))
         try:
             eng.load_state_dict(sd)
             outs.append(eng.encode_image(px).clone())
@@ -622,7 +625,7 @@ def test_ln1_rows_is_bit_identical(gpu, name, dtype, B):
     px = _pixels(B, cfg.image_size, seed=71).to(gpu)
     outs = []
     for r in (2, 1):
-        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(ln1_rows=r))
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(ln1_rows=r, attn_fuse=0))
         try:
             eng.load_state_dict(sd)
             outs.append(eng.encode_image(px).clone())
@@ -662,3 +665,44 @@ def test_blocked_qkv_h_is_bit_identical(gpu, name, dtype, B, tun):
             eng.close()
     assert torch.isfinite(outs[0]).all()
     assert torch.equal(outs[0], outs[1]), (name, dtype, B, tun)
+
+
+@pytest.mark.parametrize("dtype,B", [("fp16", 256), ("fp16", 1), ("bf16", 67)])
+def test_attention_block_fusion(gpu, dtype, B):
+    """ViT-B/32 blocks 0 .. L-2 as one kernel per image (attention + out_proj + x += y + ln_2,
+    attn_block.hip; the default) against the three-kernel path (tuning attn_fuse=0): the same
+    products in another summation order, and x + y rounded once more to the 24-bit stream, so
+    the features agree to a few fp16 ulps, not bit for bit; both against the CPU oracle at the
+    1e-3 logit bar (fp16). Per image the fused kernel is independent of the batch: image 0 of a
+    bs-B run equals the bs-1 run's bit for bit."""
+    cfg = C.get_config("ViT-B/32")
+    sd = synthetic_state_dict(cfg, 0)
+    ad = synthetic_adapters(cfg, rank=8)
+    px = _pixels(B, cfg.image_size, seed=79).to(gpu)
+    feats = {}
+    for fuse in (1, 0):
+        eng = VisionEngine(cfg, 0, dtype, max_batch=B, tuning=dict(attn_fuse=fuse))
+        try:
+            eng.load_state_dict(sd)
+            eng.load_lora(ad)
+            feats[fuse] = eng.encode_image(px).clone()
+            if fuse and B > 1:
+                one = eng.encode_image(px[:1].contiguous()).clone()
+                assert torch.equal(one[0], feats[fuse][0])
+            torch.cuda.synchronize()
+        finally:
+            eng.close()
+    f1, f0 = feats[1].float(), feats[0].float()
+    assert torch.isfinite(f1).all()
+    rel = ((f1 - f0).abs().amax(dim=1) / f0.abs().amax(dim=1)).max().item()
+    assert rel <= (2e-3 if dtype == "fp16" else 2e-2), rel
+    if dtype == "fp16":
+        ref_sd = dict(sd)
+        for a in ad:
+            ref_sd[a.target] = clip_ref.merge_lora(sd[a.target], torch.from_numpy(a.A), torch.from_numpy(a.B), a.scaling)
+        n = min(B, 4)
+        ref = clip_ref.encode_image(ref_sd, clip_ref.GEOMETRIES[cfg.name], px[:n].cpu())
+        err = [((f[:n].cpu() - ref).abs().amax(dim=1) / ref.abs().amax(dim=1)).max().item() for f in (f1, f0)]
+        assert err[0] <= 1.25 * err[1] + 1e-4, err  # fused vs the oracle: no worse than the three kernels
+        assert torch.nn.functional.cosine_similarity(f1[:n].cpu(), ref).min() > 0.9995
+
