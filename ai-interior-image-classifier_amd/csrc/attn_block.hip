@@ -222,10 +222,23 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
     }
 
     // ---------------- y = fp16(acc + b); x += y; h = LN_2(x) ----------------
+    // Row phase, as add_layernorm_kernel: wave w takes token rows t = w, w + 8, ... (< N); a lane
+    // holds columns 4 (lane + 64 i) .. + 3, i < 3, so the residual planes are read and written in
+    // whole rows and the LayerNorm statistics are wave sums (add_layernorm_kernel's arithmetic).
+    // The row loads are issued first; y goes through LDS ([64][768] fp16, the dead O image).
+    constexpr int RPW = 8;  // row slots per wave (64 token rows / 8 waves)
+    float4 xr[RPW][3];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int t = min(wave + 8 * r, N - 1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xr[r][i] = x24_load(x24, plane, (base + t) * D + (lane + 64 * i) * 4);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();  // every wave is done reading O
     // lane (j, g) of fragment (fn, fm): token t = 16 fm + j, packed row p = 96 wave + 16 fn +
     // 4 g + r -> feature n = 64 (p >> 6) + 16 g + 4 ((p >> 4) & 3) + r (the packer's permutation)
-    // (the sums x + y overwrite the accumulators: acc[fn][fm] = x + y for the LayerNorm below)
-    float ps[4] = {0.f, 0.f, 0.f, 0.f};
+    u16* Y = (u16*)smem;
 #pragma unroll
     for (int fn = 0; fn < 6; ++fn) {
         const int pr = 96 * wave + 16 * fn;
@@ -233,70 +246,33 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
         const float4 bb = *(const float4*)(bout + n);
 #pragma unroll
         for (int fm = 0; fm < 4; ++fm) {
-            const int t = min(16 * fm + j, N - 1);
-            const float4 x = x24_load(x24, plane, (base + t) * D + n);
-            const unsigned y01 = pack2<T>(acc[fn][fm][0] + bb.x, acc[fn][fm][1] + bb.y);
-            const unsigned y23 = pack2<T>(acc[fn][fm][2] + bb.z, acc[fn][fm][3] + bb.w);
-            f32x4& s4 = acc[fn][fm];
-            s4[0] = x.x + T::to_f32((u16)(y01 & 0xffff));
-            s4[1] = x.y + T::to_f32((u16)(y01 >> 16));
-            s4[2] = x.z + T::to_f32((u16)(y23 & 0xffff));
-            s4[3] = x.w + T::to_f32((u16)(y23 >> 16));
-            ps[fm] += (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            const int t = 16 * fm + j;
+            *(uint2*)(Y + t * D + n) = make_uint2(pack2<T>(acc[fn][fm][0] + bb.x, acc[fn][fm][1] + bb.y),
+                                                  pack2<T>(acc[fn][fm][2] + bb.z, acc[fn][fm][3] + bb.w));
         }
     }
-    float* red = (float*)(smem + OB);  // [8 waves][64 tokens] (the K/V stages are dead)
-    auto row_total = [&](float (&p)[4]) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            p[fm] += __shfl_xor(p[fm], 16, 64);
-            p[fm] += __shfl_xor(p[fm], 32, 64);
+    for (int r = 0; r < RPW; ++r) {
+        const int t = wave + 8 * r;
+        if (t >= N) break;
+        float4 v[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint2 w = *(const uint2*)(Y + t * D + (lane + 64 * i) * 4);
+            v[i] = xr[r][i];
+            v[i].x += T::to_f32((u16)(w.x & 0xffff));
+            v[i].y += T::to_f32((u16)(w.x >> 16));
+            v[i].z += T::to_f32((u16)(w.y & 0xffff));
+            v[i].w += T::to_f32((u16)(w.y >> 16));
+            x24_store(x24, plane, (base + t) * D + (lane + 64 * i) * 4, v[i]);
         }
-        if (g == 0) {
+        ln_row<3>(v, g2, b2, lane, (float)D);
 #pragma unroll
-            for (int fm = 0; fm < 4; ++fm) red[wave * 64 + 16 * fm + j] = p[fm];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            float t = 0.f;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) t += red[w * 64 + 16 * fm + j];
-            p[fm] = t;
-        }
-        __syncthreads();
-    };
-    row_total(ps);
-    float mean[4], pq[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm) mean[fm] = ps[fm] / (float)D;
-#pragma unroll
-    for (int fn = 0; fn < 6; ++fn)
-#pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            const f32x4 d = acc[fn][fm] - mean[fm];
-            pq[fm] += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-        }
-    row_total(pq);
-    float rstd[4];
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm) rstd[fm] = rsqrtf(pq[fm] / (float)D + 1e-5f);
-#pragma unroll
-    for (int fn = 0; fn < 6; ++fn) {
-        const int pr = 96 * wave + 16 * fn;
-        const int n = 64 * (pr >> 6) + 16 * g + 4 * ((pr >> 4) & 3);
-        const float4 gg = *(const float4*)(g2 + n), be = *(const float4*)(b2 + n);
-#pragma unroll
-        for (int fm = 0; fm < 4; ++fm) {
-            const int t = 16 * fm + j;
-            if (t >= N) continue;
-            const size_t row = base + t;
-            const float4 x = make_float4(acc[fn][fm][0], acc[fn][fm][1], acc[fn][fm][2], acc[fn][fm][3]);
-            x24_store(x24, plane, row * D + n, x);
-            const float hx = (x.x - mean[fm]) * rstd[fm] * gg.x + be.x, hy = (x.y - mean[fm]) * rstd[fm] * gg.y + be.y;
-            const float hz = (x.z - mean[fm]) * rstd[fm] * gg.z + be.z, hw = (x.w - mean[fm]) * rstd[fm] * gg.w + be.w;
-            gst<EW_AUX_ST>(hout, blk16_off((int)row, n, D), make_uint2(pack2<T>(hx, hy), pack2<T>(hz, hw)));
-        }
+        for (int i = 0; i < 3; ++i)
+            gst<EW_AUX_ST>(hout, blk16_off((int)(base + t), (lane + 64 * i) * 4, D),
+                           make_uint2(pack2<T>(v[i].x, v[i].y), pack2<T>(v[i].z, v[i].w)));
     }
 }
 
