@@ -63,13 +63,13 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
             blds16(rs, off + (unsigned)D * 2, 0, dst + 8192 + (wq * 16 + r * 8) * 128);
         }
     };
-    auto loadq = [&](int pair, vec8 (&qv)[2]) {
+    auto loadq = [&](int pair, vec8 (&qf)[2]) {
         const u16* qrow = qkv + (base + qc) * LD + (2 * pair + grp) * 64;
-        qv[0] = *(const vec8*)(qrow + 8 * g);
-        qv[1] = *(const vec8*)(qrow + 32 + 8 * g);
+        qf[0] = *(const vec8*)(qrow + 8 * g);
+        qf[1] = *(const vec8*)(qrow + 32 + 8 * g);
     };
     const float scale = 0.125f;  // 1/sqrt(64)
-    auto head = [&](int pair, const vec8 (&qv)[2]) {
+    auto head = [&](int pair, const vec8 (&qf)[2]) {
         const int h = 2 * pair + grp;
         const unsigned char* Ks = smem + OB + (pair & 1) * KVST + grp * 16384;
         const unsigned char* Vs = Ks + 8192;
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
             for (int ds = 0; ds < 2; ++ds) {
                 const int c = ((ds << 2) | g) ^ (row & 7);
                 const vec8 kf = *(const vec8*)(Ks + row * 128 + (c << 4));
-                s[kt] = T::mfma16(kf, qv[ds], s[kt]);
+                s[kt] = T::mfma16(kf, qf[ds], s[kt]);
             }
         }
         float mloc = -INFINITY;
@@ -151,69 +151,89 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
         }
     };
 
-    // out_proj interleaved with the heads: once head pair p is in the O image, its k-steps
-    // 4 p .. 4 p + 3 (O columns 128 p ..) run while pair p + 1's K / V / Q loads are in flight, so
-    // the qkv stream (HBM / Infinity Cache) and the W_out stream (L2) overlap.
-    //   y^T[n][t] = W_out[n] . O[t]: wave w owns packed W rows [96 w, 96 w + 96) (6 fragments) for
-    //   the 64 token rows (4 fragments), W fragments one k-step ahead in registers
+    // ATTB_ABL (diagnostic builds only, outputs garbage): 1 = no attention phase, 2 = no out_proj
+    // k-loop
+#ifndef ATTB_ABL
+#define ATTB_ABL 0
+#endif
+    vec8 qa[2], qb[2];
+    if constexpr (ATTB_ABL != 1) {
+    issue(0, 0);
+    loadq(0, qa);
+#pragma unroll
+    for (int pair = 0; pair < H / 2; ++pair) {
+        vec8 (&qc_)[2] = (pair & 1) ? qb : qa;
+        vec8 (&qn_)[2] = (pair & 1) ? qa : qb;
+        if (pair + 1 < H / 2) {
+            issue(pair + 1, (pair + 1) & 1);
+            loadq(pair + 1, qn_);
+            vm_wait<6>();  // this pair's 4 pieces + 2 Q loads landed; the next pair's 6 may fly
+        } else {
+            vm_wait<0>();
+        }
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of this pair
+        head(pair, qc_);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage reads and O writes
+        __builtin_amdgcn_s_barrier();        // before the stage is refilled / O is read
+    }
+    }
+
+    // ---------------- out_proj: y^T[n][t] = W_out[n] . O[t] ----------------
     const unsigned char* wl = wob + (size_t)(6 * wave) * 24576 + lane * 16;  // fragment fn: + fn * 24576
     f32x4 acc[6][4];
 #pragma unroll
     for (int fn = 0; fn < 6; ++fn)
 #pragma unroll
         for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto wload = [&](int kk, vec8 (&w)[6]) {
-#pragma unroll
-        for (int fn = 0; fn < 6; ++fn) w[fn] = *(const vec8*)(wl + fn * 24576 + (kk >> 1) * 2048 + (kk & 1) * 1024);
+    // ATTB_ROT (A/B knob): workgroup b starts its k-steps at (b * ATTB_ROT) mod 24, so the CUs of
+    // an XCD do not all read the same W_out lines at once (changes the summation order per image)
+#ifndef ATTB_ROT
+#define ATTB_ROT 0
+#endif
+    const int k0 = (int)((blockIdx.x * ATTB_ROT) % (D / 32));
+    auto wk = [&](int kk) {
+        const int k1 = kk + k0 >= D / 32 ? kk + k0 - D / 32 : kk + k0;
+        return (k1 >> 1) * 2048 + (k1 & 1) * 1024;
     };
-    auto kstep = [&](int kk, const vec8 (&w)[6]) {
+    vec8 wa[6], wb[6];
+#pragma unroll
+    for (int fn = 0; fn < 6; ++fn) wa[fn] = *(const vec8*)(wl + fn * 24576 + wk(0));
+#pragma unroll
+    for (int kk = 0; kk < (ATTB_ABL == 2 ? 0 : D / 32); ++kk) {
+        vec8 (&wc)[6] = (kk & 1) ? wb : wa;
+        vec8 (&wn)[6] = (kk & 1) ? wa : wb;
+        if (kk + 1 < D / 32) {
+            const int o1 = wk(kk + 1);
+#pragma unroll
+            for (int fn = 0; fn < 6; ++fn) wn[fn] = *(const vec8*)(wl + fn * 24576 + o1);
+        }
+        const int kr = kk + k0 >= D / 32 ? kk + k0 - D / 32 : kk + k0;
         vec8 af[4];
 #pragma unroll
         for (int fm = 0; fm < 4; ++fm) {
             const int row = 16 * fm + j;
-            const int c = (4 * kk + g) ^ j;  // (row & 15) == j
+            const int c = (4 * kr + g) ^ j;  // (row & 15) == j
             af[fm] = *(const vec8*)(smem + row * OROW + (c << 4));
         }
 #pragma unroll
         for (int fn = 0; fn < 6; ++fn)
 #pragma unroll
-            for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(w[fn], af[fm], acc[fn][fm]);
-    };
-    // vmcnt bookkeeping (in issue order; every VMEM op of a wave retires in order): pair p's K / V
-    // pieces are issued one iteration ahead, its Q loads after head p - 1, then pair p - 1's four
-    // W-fragment groups (6 loads each), then pair p + 1's 4 pieces
-    vec8 qf[2], wa[6], wb[6];
-    wload(0, wa);
-    issue(0, 0);
-    loadq(0, qf);
-#pragma unroll
-    for (int pair = 0; pair < H / 2; ++pair) {
-        if (pair + 1 < H / 2) issue(pair + 1, (pair + 1) & 1);
-        if (pair == 0) vm_wait<4>();
-        else if (pair + 1 < H / 2) vm_wait<28>();
-        else vm_wait<24>();
-        __builtin_amdgcn_s_barrier();  // every wave's pieces of this pair
-        __builtin_amdgcn_sched_barrier(0);  // (no code moves across the phases: register pressure)
-        head(pair, qf);
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage reads and O writes
-        __builtin_amdgcn_s_barrier();        // before the stage is refilled / O is read
-        if (pair + 1 < H / 2) loadq(pair + 1, qf);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int kk = 4 * pair + k;
-            if (kk + 1 < D / 32) wload(kk + 1, (kk & 1) ? wa : wb);
-            kstep(kk, (kk & 1) ? wb : wa);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+            for (int fm = 0; fm < 4; ++fm) acc[fn][fm] = T::mfma16(wc[fn], af[fm], acc[fn][fm]);
     }
 
     // ---------------- y = fp16(acc + b); x += y; h = LN_2(x) ----------------
     // Row phase, as add_layernorm_kernel: wave w takes token rows t = w, w + 8, ... (< N); a lane
     // holds columns 4 (lane + 64 i) .. + 3, i < 3, so the residual planes are read and written in
     // whole rows and the LayerNorm statistics are wave sums (add_layernorm_kernel's arithmetic).
-    // y goes through LDS ([64][768] fp16, the dead O image); the row loads are issued right after.
+    // The row loads are issued first; y goes through LDS ([64][768] fp16, the dead O image).
     constexpr int RPW = 8;  // row slots per wave (64 token rows / 8 waves)
+    float4 xr[RPW][3];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int t = min(wave + 8 * r, N - 1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) xr[r][i] = x24_load(x24, plane, (base + t) * D + (lane + 64 * i) * 4);
+    }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();  // every wave is done reading O
     // lane (j, g) of fragment (fn, fm): token t = 16 fm + j, packed row p = 96 wave + 16 fn +
@@ -230,13 +250,6 @@ __global__ __launch_bounds__(512, 1) void attn_out_ln_kernel(const u16* __restri
             *(uint2*)(Y + t * D + n) = make_uint2(pack2<T>(acc[fn][fm][0] + bb.x, acc[fn][fm][1] + bb.y),
                                                   pack2<T>(acc[fn][fm][2] + bb.z, acc[fn][fm][3] + bb.w));
         }
-    }
-    float4 xr[RPW][3];  // (after the y writes: the accumulators are dead)
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-        const int t = min(wave + 8 * r, N - 1);
-#pragma unroll
-        for (int i = 0; i < 3; ++i) xr[r][i] = x24_load(x24, plane, (base + t) * D + (lane + 64 * i) * 4);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();

@@ -1,15 +1,13 @@
 #!/bin/bash
-# r06 session 2: the fused sub-block's third form (test + A/B against the default three kernels),
-# then the closing check at HEAD: full GPU suite, smoke(), default bench line
+# r06 session 2: the closing check at HEAD (full GPU suite, smoke(), default bench line), then the
+# fused sub-block's third form (test + A/B against the default three kernels)
 set -o pipefail
 O=gpurun_out/c23
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -s -k "fusion" --timeout 300 --timeout-method thread > $O/fuse_tests.log 2>&1 || { echo "fusion tests failed"; tail -40 $O/fuse_tests.log; exit 1; }
-tail -2 $O/fuse_tests.log
-bash tools/ab_envs.sh "--steps 20 --warmup 5" 3 - "--tuning attn_fuse=1" > $O/fuse_ab.log 2>&1
-cat $O/fuse_ab.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "gpu tests failed"; tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" || { echo "smoke failed"; exit 1; }
 timeout -k 10 400 python -u bench.py > $O/default.json 2> $O/default.err || { echo "bench failed"; tail -20 $O/default.err; exit 1; }
-head -c 700 $O/default.json
+head -c 400 $O/default.json; echo
+bash tools/ab_envs.sh "--steps 20 --warmup 5" 3 - "--tuning attn_fuse=1" > $O/fuse_ab.log 2>&1
+cat $O/fuse_ab.log
