@@ -103,13 +103,16 @@ int clipvit_create(const clipvit_config* cfg, int device, clipvit_handle** out);
  * split_variants "main,tail"; tail_variant; tail_kmin (>= 64, multiple of 64) / tail_smax (1..48):
  * the class-token tail's split-K rule; head_cols (64 / 32); mx8_split_tail (0, 2, 5);
  * split_xcd; max_inflight; split_min (<= 0: never split); gemm_xcd / gemm_variants "q,o,f,p,e";
- * qkv_variant / fc_variant (100 * XCD map + tile of the QKV / c_fc role only); fc_balanced (0/1:
+ * qkv_variant / fc_variant / out_variant / proj_variant (100 * XCD map + tile of that role only;
+ * 79 = the 192 x 256 persistent tile for out_proj / c_proj); fc_balanced (0/1:
  * c_fc with >= 2 whole rounds of 256x256 tiles plus a remainder as one balanced launch, default 1,
  * or as the round split of split_variants); fc_balanced_variant (75 / 77: its tile);
  * h_blocked (0..3: ln_2 writes c_fc's A in the 16-row blocked layout by direct stores (1) or an
  * LDS transpose of 16-row (2) or 8-row (3, default) groups per workgroup); patch_im2col (0/1: the pixel cast writes a blocked im2col matrix
  * for an explicit patch GEMM, default 1; 0 = the implicit GEMM over the cast pixels);
  * ln1_rows (1/2: rows per wave of the add + LayerNorm after c_proj, default 1); attn_persist (0..4: N <= 64 attention as a persistent loop on that many workgroups per CU);
+ * attn_fuse (0/1: ViT-B/32 blocks 0 .. L-2 as one attention + out_proj + add + ln_2 kernel per
+ * image, default 0);
  * trace_gemm (0/1: clipvit_gemm_log);
  * large_variants "q,f,o,p"; mx8_variants "q,o,f,p" (3 = ping-pong 256x256, 4 = the 32x32x64 scaled-MFMA
  * form of the 32-deep-k-step tile, QKV / c_fc only); mx8_skip / mx8_skip_mlp "i,j,.." (bf16
